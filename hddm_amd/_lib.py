@@ -1,0 +1,180 @@
+"""ctypes binding to libwfpt_amd.so (include/wfpt_amd.h).
+
+There is no CPU fallback: if the HIP library is missing this module raises
+ImportError, and every device/driver failure raises RuntimeError with the
+library's message (never a numeric stand-in).
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("WFPT_AMD_LIB", os.path.join(_PKG, "lib", "libwfpt_amd.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"hddm_amd: HIP library not found at {LIB_PATH}; build it with "
+        "`python -m hddm_amd.build` (hipcc --offload-arch=gfx950)")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+WFPT_OK = 0
+WFPT_MAX_DEPTH = 24
+
+_D = ctypes.c_double
+_I = ctypes.c_int
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_PD = ctypes.POINTER(ctypes.c_double)
+_VP = ctypes.c_void_p
+
+
+class Params(ctypes.Structure):
+    _fields_ = [(n, _D) for n in ("v", "sv", "a", "z", "sz", "t", "st", "p_outlier")]
+
+
+class Knobs(ctypes.Structure):
+    _fields_ = [("err", _D), ("n_st", _I32), ("n_sz", _I32), ("use_adaptive", _I32),
+                ("simps_err", _D), ("w_outlier", _D)]
+
+
+_PP = ctypes.POINTER(Params)
+_PK = ctypes.POINTER(Knobs)
+
+
+def _sig(name, res, args):
+    f = getattr(_lib, name)
+    f.restype = res
+    f.argtypes = args
+    return f
+
+
+wfpt_last_error = _sig("wfpt_last_error", ctypes.c_char_p, [])
+wfpt_device_count = _sig("wfpt_device_count", _I, [ctypes.POINTER(_I)])
+wfpt_open = _sig("wfpt_open", _I, [_I, ctypes.POINTER(_VP)])
+wfpt_close = _sig("wfpt_close", None, [_VP])
+wfpt_dataset_create = _sig("wfpt_dataset_create", _I,
+                           [_VP, _PD, _I64, ctypes.POINTER(_I32), _I32, ctypes.POINTER(_VP)])
+wfpt_dataset_destroy = _sig("wfpt_dataset_destroy", None, [_VP])
+wfpt_dataset_size = _sig("wfpt_dataset_size", _I64, [_VP])
+wfpt_shard_range = _sig("wfpt_shard_range", None,
+                        [_I64, _I, _I, ctypes.POINTER(_I64), ctypes.POINTER(_I64)])
+wfpt_wiener_like = _sig("wfpt_wiener_like", _I, [_VP, _VP, _PP, _PK, _PD])
+wfpt_wiener_like_host = _sig("wfpt_wiener_like_host", _I, [_VP, _PD, _I64, _PP, _PK, _PD])
+wfpt_wiener_like_nodes = _sig("wfpt_wiener_like_nodes", _I, [_VP, _VP, _PP, _PK, _PD])
+wfpt_pdf_array = _sig("wfpt_pdf_array", _I, [_VP, _PD, _I64, _PP, _PK, _I, _PD])
+wfpt_full_pdf = _sig("wfpt_full_pdf", _I, [_VP, _D, _PP, _PK, _PD])
+wfpt_wiener_like_multi = _sig("wfpt_wiener_like_multi", _I,
+                              [_VP, _PD, _I64, ctypes.POINTER(_PD), _PD, _PK, _D, _PD])
+wfpt_comm_unique_id = _sig("wfpt_comm_unique_id", _I, [ctypes.c_char_p])
+wfpt_comm_init = _sig("wfpt_comm_init", _I, [_VP, _I, _I, ctypes.c_char_p])
+wfpt_wiener_like_allreduce = _sig("wfpt_wiener_like_allreduce", _I, [_VP, _VP, _PP, _PK, _PD])
+wfpt_profile_enable = _sig("wfpt_profile_enable", _I, [_VP, _I])
+wfpt_profile_read = _sig("wfpt_profile_read", _I,
+                         [_VP, _PD, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I])
+wfpt_synchronize = _sig("wfpt_synchronize", _I, [_VP])
+
+EXPORTED = [
+    "wfpt_device_count", "wfpt_open", "wfpt_close", "wfpt_last_error", "wfpt_dataset_create",
+    "wfpt_dataset_destroy", "wfpt_dataset_size", "wfpt_shard_range", "wfpt_wiener_like",
+    "wfpt_wiener_like_host", "wfpt_wiener_like_nodes", "wfpt_pdf_array", "wfpt_full_pdf",
+    "wfpt_wiener_like_multi", "wfpt_comm_unique_id", "wfpt_comm_init",
+    "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
+]
+
+
+def check(rc):
+    if rc != WFPT_OK:
+        msg = wfpt_last_error().decode(errors="replace")
+        if rc == 4:
+            raise NotImplementedError(f"wfpt_amd: {msg}")
+        if rc == 2:
+            raise ValueError(f"wfpt_amd: {msg}")
+        raise RuntimeError(f"wfpt_amd error {rc}: {msg}")
+
+
+def dptr(a):
+    return a.ctypes.data_as(_PD)
+
+
+class Context:
+    """One HIP device + stream + workspaces (wfpt_ctx)."""
+
+    def __init__(self, device=0):
+        h = _VP()
+        check(wfpt_open(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = int(device)
+
+    def close(self):
+        if self.handle:
+            wfpt_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    PROF_EVENTS = 1
+    PROF_EVALS = 2
+
+    def profile(self, flags=1):
+        """flags: PROF_EVENTS (per-launch HIP-event time) | PROF_EVALS (count pdf_sv evals)."""
+        check(wfpt_profile_enable(self.handle, int(flags)))
+
+    def profile_read(self, reset=False):
+        ms, nl, ne = _D(), _I64(), _I64()
+        check(wfpt_profile_read(self.handle, ctypes.byref(ms), ctypes.byref(nl),
+                                ctypes.byref(ne), 1 if reset else 0))
+        return ms.value, nl.value, ne.value
+
+    def synchronize(self):
+        check(wfpt_synchronize(self.handle))
+
+
+_ctx_lock = threading.Lock()
+_contexts = {}
+
+
+def default_device():
+    env = os.environ.get("WFPT_DEVICE")
+    if env is not None:
+        return int(env)
+    return 0
+
+
+def context(device=None):
+    """Process-wide context for `device` (default: $WFPT_DEVICE or 0)."""
+    dev = default_device() if device is None else int(device)
+    with _ctx_lock:
+        c = _contexts.get(dev)
+        if c is None:
+            c = Context(dev)
+            _contexts[dev] = c
+        return c
+
+
+def device_count():
+    n = _I()
+    check(wfpt_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def shard_range(n, nranks, rank):
+    lo, hi = _I64(), _I64()
+    wfpt_shard_range(int(n), int(nranks), int(rank), ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def make_params(v, sv, a, z, sz, t, st, p_outlier=0.0):
+    return Params(float(v), float(sv), float(a), float(z), float(sz), float(t), float(st),
+                  float(p_outlier))
+
+
+def make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier):
+    return Knobs(float(err), int(n_st), int(n_sz), 1 if use_adaptive else 0, float(simps_err),
+                 float(w_outlier))

@@ -1,0 +1,60 @@
+"""Build libwfpt_amd.so in-tree (hipcc, gfx950 only).
+
+    python -m hddm_amd.build [--force]
+
+The library lands in hddm_amd/lib/ (git-ignored, shipped to the GPU box with
+the working tree). No CMake, no JIT cache: the .so that the tests and bench
+load is exactly the one built here.
+"""
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+LIB = os.path.join(LIBDIR, "libwfpt_amd.so")
+SOURCES = ["wfpt_kernels.hip", "wfpt_capi.cpp"]
+DEPS = SOURCES + ["wfpt_device.hpp", "wfpt_internal.h"]
+ARCH = os.environ.get("WFPT_OFFLOAD_ARCH", "gfx950")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
+          f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    os.makedirs(LIBDIR, exist_ok=True)
+    deps = [os.path.join(CSRC, f) for f in DEPS] + [os.path.join(ROOT, "include", "wfpt_amd.h")]
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
+        cmd = [HIPCC, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB + ".tmp"
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
+           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    for o in objs:
+        os.remove(o)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

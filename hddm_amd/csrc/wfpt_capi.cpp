@@ -1,0 +1,597 @@
+// wfpt_capi.cpp — C ABI of the MI355X WFPT engine (include/wfpt_amd.h).
+//
+// Host runtime: one context per GPU (HIP stream, grow-only device workspaces,
+// pinned result slot, optional RCCL communicator), resident datasets, and the
+// call sequences  trial kernel -> finalize -> 16-byte D2H  per likelihood.
+// Calls into one context are serialised by its mutex; the ctypes binding
+// releases the GIL around every call.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/wfpt_amd.h"
+#include "wfpt_device.hpp"
+#include "wfpt_internal.h"
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      return fail(WFPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                 \
+  do {                                                                                 \
+    ncclResult_t r_ = (expr);                                                          \
+    if (r_ != ncclSuccess)                                                             \
+      return fail(WFPT_ERR_COMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 256);
+    hipError_t e = hipMalloc((void**)&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct wfpt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf<double> x;       // uploads of host arrays
+  DevBuf<double> part;    // block partial sums
+  DevBuf<int> zero;       // block zero counts
+  DevBuf<double> res;     // final {sum, zeros} or per-node results
+  DevBuf<double> lp;      // per-trial outputs
+  DevBuf<wfpt::Params> nodep;
+  DevBuf<double> marr;    // wiener_like_multi parameter arrays
+  DevBuf<double*> mptr;
+  DevBuf<double> mscal;
+  unsigned long long* evals = nullptr;
+  int* status = nullptr;      // device: Simpson-stack overflow flag
+  int* host_status = nullptr; // pinned mirror
+  double* host = nullptr;  // pinned result slot
+  size_t host_cap = 0;
+  bool profile = false;      // HIP events around the main kernel
+  bool count = false;        // pdf_sv evaluation counting
+  double k_ms = 0.0;
+  int64_t launches = 0;
+  int64_t n_evals = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+struct wfpt_ds {
+  wfpt_ctx* ctx = nullptr;
+  int64_t n = 0;
+  double* x = nullptr;
+  int32_t* node = nullptr;
+  int64_t* off = nullptr;
+  int32_t n_nodes = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    (void)hipGetDevice(&prev);
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+wfpt::Params to_params(const wfpt_params* p) {
+  wfpt::Params q;
+  q.v = p->v;
+  q.sv = p->sv;
+  q.a = p->a;
+  q.z = p->z;
+  q.sz = p->sz;
+  q.t = p->t;
+  q.st = p->st;
+  q.p_outlier = p->p_outlier;
+  return q;
+}
+
+wfpt::Knobs to_knobs(const wfpt_knobs* k) {
+  wfpt::Knobs q;
+  q.err = k->err;
+  q.n_st = k->n_st;
+  q.n_sz = k->n_sz;
+  q.use_adaptive = k->use_adaptive != 0;  // `bint` in the reference signatures
+  q.simps_err = k->simps_err;
+  q.w_outlier = k->w_outlier;
+  return q;
+}
+
+bool p_outlier_in_range(double p) { return (p >= 0) & (p <= 1); }  // wfpt.pyx:50-51
+
+int ensure_host(wfpt_ctx* c, size_t n) {
+  if (n <= c->host_cap) return WFPT_OK;
+  if (c->host) (void)hipHostFree(c->host);
+  c->host = nullptr;
+  HIP_TRY(hipHostMalloc((void**)&c->host, n * sizeof(double), hipHostMallocDefault));
+  c->host_cap = n;
+  return WFPT_OK;
+}
+
+// Runs the trial kernel (block sums) + finalize on device x[n]; leaves
+// {sum, zeros} in c->res.p[0..1] (device). Records profile events.
+// Zero the overflow flag before a launch; check it after the stream sync.
+int begin_status(wfpt_ctx* c) {
+  HIP_TRY(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+  return WFPT_OK;
+}
+int fetch_status(wfpt_ctx* c) {
+  HIP_TRY(hipMemcpyAsync(c->host_status, c->status, sizeof(int), hipMemcpyDeviceToHost,
+                         c->stream));
+  return WFPT_OK;
+}
+int check_status(wfpt_ctx* c) {
+  if (*c->host_status)
+    return fail(WFPT_ERR_UNSUPPORTED,
+                "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
+                    std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)");
+  return WFPT_OK;
+}
+
+int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
+            const wfpt::Knobs& K) {
+  const int64_t nb = wfpt::blocks_for(n);
+  if (int rc = begin_status(c)) return rc;
+  HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
+  HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
+  HIP_TRY(c->res.reserve(2));
+  if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  wfpt::launch_trials(0, dx, n, P, K, c->part.p, c->zero.p, c->count ? c->evals : nullptr,
+                      c->status, 0, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  if (nb > 0) {
+    wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->res.p, c->stream);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemsetAsync(c->res.p, 0, 2 * sizeof(double), c->stream));
+  }
+  return WFPT_OK;
+}
+
+int finish_profile(wfpt_ctx* c) {
+  if (c->profile) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->k_ms += ms;
+    c->launches += 1;
+  }
+  if (c->count) {
+    unsigned long long ev = 0;
+    HIP_TRY(hipMemcpy(&ev, c->evals, sizeof(ev), hipMemcpyDeviceToHost));
+    c->n_evals += (int64_t)ev;
+  }
+  return WFPT_OK;
+}
+
+int read_sum(wfpt_ctx* c, double* out) {
+  int rc = ensure_host(c, 2);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream));
+  if ((rc = fetch_status(c))) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if ((rc = check_status(c))) return rc;
+  rc = finish_profile(c);
+  if (rc) return rc;
+  *out = (c->host[1] > 0) ? -INFINITY : c->host[0];
+  return WFPT_OK;
+}
+
+int upload(wfpt_ctx* c, const double* x, int64_t n) {
+  HIP_TRY(c->x.reserve(std::max<int64_t>(n, 1)));
+  if (n > 0)
+    HIP_TRY(hipMemcpyAsync(c->x.p, x, n * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  return WFPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* wfpt_last_error(void) { return g_last_error.c_str(); }
+
+int wfpt_device_count(int* n) {
+  if (!n) return fail(WFPT_ERR_ARG, "null pointer");
+  HIP_TRY(hipGetDeviceCount(n));
+  return WFPT_OK;
+}
+
+int wfpt_open(int device, wfpt_ctx** out) {
+  if (!out) return fail(WFPT_ERR_ARG, "null pointer");
+  int nd = 0;
+  HIP_TRY(hipGetDeviceCount(&nd));
+  if (device < 0 || device >= nd)
+    return fail(WFPT_ERR_ARG, "device " + std::to_string(device) + " not present (" +
+                                  std::to_string(nd) + " visible)");
+  DeviceGuard g(device);
+  HIP_TRY(hipSetDevice(device));
+  auto* c = new wfpt_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->evals, sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->status, sizeof(int));
+  if (e == hipSuccess) e = hipHostMalloc((void**)&c->host_status, sizeof(int), hipHostMallocDefault);
+  if (e != hipSuccess) {
+    wfpt_close(c);
+    return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
+  }
+  *out = c;
+  return WFPT_OK;
+}
+
+void wfpt_close(wfpt_ctx* c) {
+  if (!c) return;
+  DeviceGuard g(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  c->x.release();
+  c->part.release();
+  c->zero.release();
+  c->res.release();
+  c->lp.release();
+  c->nodep.release();
+  c->marr.release();
+  c->mptr.release();
+  c->mscal.release();
+  if (c->evals) (void)hipFree(c->evals);
+  if (c->status) (void)hipFree(c->status);
+  if (c->host_status) (void)hipHostFree(c->host_status);
+  if (c->host) (void)hipHostFree(c->host);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+void wfpt_shard_range(int64_t n, int nranks, int rank, int64_t* lo, int64_t* hi) {
+  if (nranks < 1) nranks = 1;
+  const int64_t base = n / nranks, rem = n % nranks;
+  const int64_t l = rank * base + std::min<int64_t>(rank, rem);
+  *lo = l;
+  *hi = l + base + (rank < rem ? 1 : 0);
+}
+
+int wfpt_dataset_create(wfpt_ctx* c, const double* rt, int64_t n, const int32_t* node_id,
+                        int32_t n_nodes, wfpt_ds** out) {
+  if (!c || !out || (n > 0 && !rt) || n < 0) return fail(WFPT_ERR_ARG, "bad dataset arguments");
+  if (node_id && n_nodes <= 0) return fail(WFPT_ERR_ARG, "node ids need n_nodes > 0");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  // host-side layout: group by node, order by |rt| inside a node so that each
+  // wavefront sees one series branch / similar quadrature depth.
+  const bool keep_order = std::getenv("WFPT_DATASET_ORDER") &&
+                          std::strcmp(std::getenv("WFPT_DATASET_ORDER"), "input") == 0;
+  std::vector<int64_t> idx(n);
+  for (int64_t i = 0; i < n; ++i) idx[i] = i;
+  std::vector<int64_t> off;
+  if (node_id) {
+    for (int64_t i = 0; i < n; ++i)
+      if (node_id[i] < 0 || node_id[i] >= n_nodes)
+        return fail(WFPT_ERR_ARG, "node id out of range at trial " + std::to_string(i));
+    std::vector<int64_t> cnt(n_nodes + 1, 0);
+    for (int64_t i = 0; i < n; ++i) cnt[node_id[i] + 1]++;
+    for (int32_t j = 0; j < n_nodes; ++j) cnt[j + 1] += cnt[j];
+    off = cnt;
+    std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
+    for (int64_t i = 0; i < n; ++i) idx[pos[node_id[i]]++] = i;
+    if (!keep_order)
+      for (int32_t j = 0; j < n_nodes; ++j)
+        std::stable_sort(idx.begin() + off[j], idx.begin() + off[j + 1],
+                         [&](int64_t a, int64_t b) { return std::fabs(rt[a]) < std::fabs(rt[b]); });
+  } else if (!keep_order) {
+    std::stable_sort(idx.begin(), idx.end(),
+                     [&](int64_t a, int64_t b) { return std::fabs(rt[a]) < std::fabs(rt[b]); });
+  }
+  std::vector<double> hx(n);
+  std::vector<int32_t> hn(node_id ? n : 0);
+  for (int64_t i = 0; i < n; ++i) {
+    hx[i] = rt[idx[i]];
+    if (node_id) hn[i] = node_id[idx[i]];
+  }
+  auto* d = new wfpt_ds();
+  d->ctx = c;
+  d->n = n;
+  d->n_nodes = node_id ? n_nodes : 0;
+  hipError_t e = hipMalloc((void**)&d->x, std::max<int64_t>(n, 1) * sizeof(double));
+  if (e == hipSuccess && n > 0)
+    e = hipMemcpy(d->x, hx.data(), n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess && node_id) {
+    e = hipMalloc((void**)&d->node, std::max<int64_t>(n, 1) * sizeof(int32_t));
+    if (e == hipSuccess && n > 0)
+      e = hipMemcpy(d->node, hn.data(), n * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc((void**)&d->off, (n_nodes + 1) * sizeof(int64_t));
+    if (e == hipSuccess)
+      e = hipMemcpy(d->off, off.data(), (n_nodes + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) {
+    wfpt_dataset_destroy(d);
+    return fail(WFPT_ERR_HIP, std::string("wfpt_dataset_create: ") + hipGetErrorString(e));
+  }
+  *out = d;
+  return WFPT_OK;
+}
+
+void wfpt_dataset_destroy(wfpt_ds* d) {
+  if (!d) return;
+  DeviceGuard g(d->ctx ? d->ctx->device : 0);
+  if (d->x) (void)hipFree(d->x);
+  if (d->node) (void)hipFree(d->node);
+  if (d->off) (void)hipFree(d->off);
+  delete d;
+}
+
+int64_t wfpt_dataset_size(const wfpt_ds* d) { return d ? d->n : -1; }
+
+int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const wfpt_knobs* k,
+                     double* out) {
+  if (!c || !d || !p || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (!p_outlier_in_range(P.p_outlier)) {  // wfpt.pyx:63-64
+    *out = -INFINITY;
+    return WFPT_OK;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = run_sum(c, d->x, d->n, P, K)) return rc;
+  return read_sum(c, out);
+}
+
+int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
+                          const wfpt_knobs* k, double* out) {
+  if (!c || (!x && n > 0) || !p || !k || !out || n < 0) return fail(WFPT_ERR_ARG, "bad arguments");
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (!p_outlier_in_range(P.p_outlier)) {
+    *out = -INFINITY;
+    return WFPT_OK;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = upload(c, x, n)) return rc;
+  if (int rc = run_sum(c, c->x.p, n, P, K)) return rc;
+  return read_sum(c, out);
+}
+
+int wfpt_pdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
+                   const wfpt_knobs* k, int logp, double* out) {
+  if (!c || (!x && n > 0) || !p || !k || (!out && n > 0) || n < 0)
+    return fail(WFPT_ERR_ARG, "bad arguments");
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (n == 0) return WFPT_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = upload(c, x, n)) return rc;
+  HIP_TRY(c->lp.reserve(n));
+  if (int rc = begin_status(c)) return rc;
+  wfpt::launch_trials(1, c->x.p, n, P, K, c->lp.p, nullptr, nullptr, c->status, logp == 1,
+                      c->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (int rc = fetch_status(c)) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return check_status(c);
+}
+
+int wfpt_full_pdf(wfpt_ctx* c, double x, const wfpt_params* p, const wfpt_knobs* k,
+                  double* out) {
+  if (!p || !k) return fail(WFPT_ERR_ARG, "null pointer");
+  wfpt_params q = *p;
+  q.p_outlier = 0.0;
+  wfpt_knobs kk = *k;
+  kk.w_outlier = 0.0;
+  return wfpt_pdf_array(c, &x, 1, &q, &kk, 0, out);
+}
+
+int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
+                           const wfpt_knobs* k, double* out) {
+  if (!c || !d || !per_node || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  if (!d->node) return fail(WFPT_ERR_ARG, "dataset was created without node ids");
+  const wfpt::Knobs K = to_knobs(k);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const int32_t m = d->n_nodes;
+  std::vector<wfpt::Params> hp(m);
+  for (int32_t j = 0; j < m; ++j) hp[j] = to_params(&per_node[j]);
+  HIP_TRY(c->nodep.reserve(m));
+  HIP_TRY(hipMemcpyAsync(c->nodep.p, hp.data(), m * sizeof(wfpt::Params), hipMemcpyHostToDevice,
+                         c->stream));
+  HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
+  HIP_TRY(c->res.reserve(m));
+  if (int rc = begin_status(c)) return rc;
+  if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  wfpt::launch_nodes(d->x, d->node, d->n, c->nodep.p, K, c->lp.p,
+                     c->count ? c->evals : nullptr, c->status, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (int rc = ensure_host(c, m)) return rc;
+  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, m * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream));
+  if (int rc = fetch_status(c)) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int rc = check_status(c)) return rc;
+  if (int rc = finish_profile(c)) return rc;
+  std::memcpy(out, c->host, m * sizeof(double));
+  return WFPT_OK;
+}
+
+int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
+                           const double* const arrays[7], const double scalars[7],
+                           const wfpt_knobs* k, double p_outlier, double* out) {
+  if (!c || (!x && n > 0) || !arrays || !scalars || !k || !out || n < 0)
+    return fail(WFPT_ERR_ARG, "bad arguments");
+  const wfpt::Knobs K = to_knobs(k);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = upload(c, x, n)) return rc;
+  int na = 0;
+  for (int j = 0; j < 7; ++j) na += arrays[j] != nullptr;
+  HIP_TRY(c->marr.reserve(std::max<int64_t>((int64_t)na * n, 1)));
+  HIP_TRY(c->mptr.reserve(7));
+  HIP_TRY(c->mscal.reserve(7));
+  double* hptr[7];
+  int slot = 0;
+  for (int j = 0; j < 7; ++j) {
+    if (arrays[j]) {
+      hptr[j] = c->marr.p + (int64_t)slot * n;
+      if (n > 0)
+        HIP_TRY(hipMemcpyAsync(hptr[j], arrays[j], n * sizeof(double), hipMemcpyHostToDevice,
+                               c->stream));
+      ++slot;
+    } else {
+      hptr[j] = nullptr;
+    }
+  }
+  HIP_TRY(hipMemcpyAsync(c->mptr.p, hptr, sizeof(hptr), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->mscal.p, scalars, 7 * sizeof(double), hipMemcpyHostToDevice,
+                         c->stream));
+  const int64_t nb = wfpt::blocks_for(n);
+  HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
+  HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
+  HIP_TRY(c->res.reserve(2));
+  if (int rc = begin_status(c)) return rc;
+  wfpt::launch_multi(c->x.p, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
+                     c->status, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (nb > 0) {
+    wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->res.p, c->stream);
+    HIP_TRY(hipGetLastError());
+  } else {
+    HIP_TRY(hipMemsetAsync(c->res.p, 0, 2 * sizeof(double), c->stream));
+  }
+  if (int rc = ensure_host(c, 2)) return rc;
+  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, 2 * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream));
+  if (int rc = fetch_status(c)) return rc;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int rc = check_status(c)) return rc;
+  *out = c->host[0];
+  return WFPT_OK;
+}
+
+int wfpt_comm_unique_id(unsigned char id[128]) {
+  if (!id) return fail(WFPT_ERR_ARG, "null pointer");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId u;
+  NCCL_TRY(ncclGetUniqueId(&u));
+  std::memcpy(id, &u, 128);
+  return WFPT_OK;
+}
+
+int wfpt_comm_init(wfpt_ctx* c, int nranks, int rank, const unsigned char id[128]) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(WFPT_ERR_ARG, "bad communicator arguments");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  HIP_TRY(hipSetDevice(c->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, 128);
+  if (c->comm) {
+    (void)ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  NCCL_TRY(ncclCommInitRank(&c->comm, nranks, u, rank));
+  c->nranks = nranks;
+  c->rank = rank;
+  return WFPT_OK;
+}
+
+int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
+                               const wfpt_knobs* k, double* out) {
+  if (!c || !d || !p || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (!c->comm) return fail(WFPT_ERR_ARG, "wfpt_comm_init was not called");
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (!p_outlier_in_range(P.p_outlier)) {  // uniform on every rank: no exchange needed
+    *out = -INFINITY;
+    return WFPT_OK;
+  }
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = run_sum(c, d->x, d->n, P, K)) return rc;
+  NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 2, ncclDouble, ncclSum, c->comm, c->stream));
+  return read_sum(c, out);
+}
+
+int wfpt_profile_enable(wfpt_ctx* c, int flags) {
+  if (!c) return fail(WFPT_ERR_ARG, "null pointer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->profile = (flags & WFPT_PROF_EVENTS) != 0;
+  c->count = (flags & WFPT_PROF_EVALS) != 0;
+  return WFPT_OK;
+}
+
+int wfpt_profile_read(wfpt_ctx* c, double* kernel_ms, int64_t* launches, int64_t* n_evals,
+                      int reset) {
+  if (!c) return fail(WFPT_ERR_ARG, "null pointer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  if (kernel_ms) *kernel_ms = c->k_ms;
+  if (launches) *launches = c->launches;
+  if (n_evals) *n_evals = c->n_evals;
+  if (reset) {
+    c->k_ms = 0.0;
+    c->launches = 0;
+    c->n_evals = 0;
+  }
+  return WFPT_OK;
+}
+
+int wfpt_synchronize(wfpt_ctx* c) {
+  if (!c) return fail(WFPT_ERR_ARG, "null pointer");
+  DeviceGuard g(c->device);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return WFPT_OK;
+}
+
+}  // extern "C"

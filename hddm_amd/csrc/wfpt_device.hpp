@@ -1,0 +1,436 @@
+// wfpt_device.hpp — device-side WFPT density for gfx950 (CDNA4), fp64.
+//
+// Restates the reference's numerics (src/pdf.pxi:28-146, src/integrate.pxi:12-206)
+// for one-trial-per-lane execution:
+//   * every *decision* (series branch, term count K, adaptive stop test, node
+//     coordinates) is computed with the same IEEE operations in the same order
+//     as the reference, so the quadrature tree is identical;
+//   * work that depends only on the non-decision time node t (the series
+//     branch and K, sqrt/log terms, sv normalisers) is hoisted out of the z
+//     integral: one `TNode` per t node serves all z nodes;
+//   * the reference's recursion becomes an explicit per-lane stack (registers
+//     for depth <= 4, scratch beyond) driven by a loop with a single
+//     evaluation site, so divergent refinement does not duplicate code.
+// Compiled with -ffp-contract=off: no FMA contraction, like the x86-64 build
+// of the reference.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace wfpt {
+
+constexpr double kPi = 3.14159265358979323846;  // M_PI
+constexpr double kPi2 = kPi * kPi;             // M_PI**2 (pdf.pxi:37, 62)
+
+struct Params {
+  double v, sv, a, z, sz, t, st, p_outlier;
+};
+struct Knobs {
+  double err;
+  int n_st, n_sz, use_adaptive;
+  double simps_err, w_outlier;
+};
+
+enum Mode : int {
+  kDirect = 0,   // sz = st = 0: one pdf_sv (pdf.pxi:129)
+  kAdaptT = 1,   // st only, adaptive (pdf.pxi:132)
+  kAdaptZ = 2,   // sz only, adaptive (pdf.pxi:139)
+  kAdaptTZ = 3,  // sz and st, adaptive 2-D (pdf.pxi:144)
+  kFixedT = 4,   // fixed Simpson variants (pdf.pxi:134, 141, 146)
+  kFixedZ = 5,
+  kFixedTZ = 6,
+  kRuntime = 7,  // per-trial parameters: mode decided per lane
+};
+
+// Host+device: mode after full_pdf's st/sz < 1e-3 zeroing (pdf.pxi:122-146).
+__host__ __device__ inline int select_mode(double sz, double st, int use_adaptive) {
+  const bool zst = !(st >= 1e-3), zsz = !(sz >= 1e-3);
+  if (zsz) {
+    if (zst) return kDirect;
+    return use_adaptive > 0 ? kAdaptT : kFixedT;
+  }
+  if (zst) return use_adaptive ? kAdaptZ : kFixedZ;
+  return use_adaptive ? kAdaptTZ : kFixedTZ;
+}
+
+// ---------------------------------------------------------------------------
+// Per-t-node quantities of ftt_01w / pdf_sv that do not depend on w (= z).
+struct TNode {
+  double xx;    // x - t_node: the `x` argument of pdf_sv
+  double tt;    // xx / a^2 (pdf.pxi:98)
+  double norm;  // small-t: sqrt(2*pi*tt^3) divisor (pdf.pxi:57)
+  double den;   // sv: 2*sv^2*xx + 2   (pdf.pxi:102)
+  double sq;    // sv: sqrt(sv^2*xx + 1)
+  double vvx;   // v^2 * xx
+  int K;        // number of series terms (pdf.pxi:52, 60)
+  int small;    // 1 => small-time series
+  int pos;      // xx > 0 (else density 0, pdf.pxi:92)
+};
+
+__device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err) {
+  TNode T;
+  T.xx = xx;
+  T.pos = xx > 0;
+  T.tt = 0.0;
+  T.norm = 1.0;
+  T.den = 1.0;
+  T.sq = 1.0;
+  T.vvx = 0.0;
+  T.K = 0;
+  T.small = 0;
+  if (!T.pos) return T;
+  const double tt = xx / (a * a);
+  T.tt = tt;
+  double kl, ks;
+  // pdf.pxi:36-40
+  if ((kPi * tt) * err < 1.0) {
+    kl = sqrt((-2.0 * log((kPi * tt) * err)) / (kPi2 * tt));
+    const double b = 1. / (kPi * sqrt(tt));
+    kl = (kl < b) ? b : kl;
+  } else {
+    kl = 1. / (kPi * sqrt(tt));
+  }
+  // pdf.pxi:43-47
+  const double s2pt = sqrt((2.0 * kPi) * tt);
+  if ((2.0 * s2pt) * err < 1.0) {
+    ks = 2.0 + sqrt((-2.0 * tt) * log((2.0 * s2pt) * err));
+    const double b = sqrt(tt) + 1.0;
+    ks = (ks < b) ? b : ks;
+  } else {
+    ks = 2.0;
+  }
+  if (ks < kl) {
+    T.small = 1;
+    T.K = (int)ceil(ks);
+    T.norm = sqrt((2.0 * kPi) * pow(tt, 3.0));
+  } else {
+    T.small = 0;
+    T.K = (int)ceil(kl);
+  }
+  if (sv != 0) {
+    T.den = ((2.0 * (sv * sv)) * xx) + 2.0;
+    T.sq = sqrt(((sv * sv) * xx) + 1.0);
+  }
+  T.vvx = (v * v) * xx;
+  return T;
+}
+
+// f(t|0,1,w) from a prepared t node (pdf.pxi:49-65).
+__device__ inline double tnode_ftt(const TNode& T, double w) {
+  double p = 0.0;
+  if (T.small) {
+    const int K = T.K;
+    const int lower = (int)(-floor((K - 1) / 2.));
+    const int upper = (int)ceil((K - 1) / 2.);
+    for (int k = lower; k <= upper; ++k) {
+      const double wk = w + (double)(2 * k);
+      p = p + wk * exp(((-(wk * wk)) / 2.0) / T.tt);
+    }
+    p = p / T.norm;
+  } else {
+    const int K = T.K;
+    for (int k = 1; k <= K; ++k) {
+      const double dk = (double)k;
+      p = p + (dk * exp((((-(dk * dk)) * kPi2) * T.tt) / 2.0)) * sin((dk * kPi) * w);
+    }
+    p = p * kPi;
+  }
+  return p;
+}
+
+// pdf_sv(xx, v, sv, a, w, err) (pdf.pxi:74-102) from a prepared t node.
+__device__ inline double tnode_pdf_sv(const TNode& T, double w, double v, double sv, double a) {
+  if (!T.pos) return 0.0;
+  const double p = tnode_ftt(T, w);
+  if (sv == 0) return (p * exp((((-v) * a) * w) - (T.vvx / 2.))) / (a * a);
+  const double azsv = (a * w) * sv;
+  return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) / T.den) / T.sq) /
+         (a * a);
+}
+
+__device__ inline double pdf_sv(double xx, double v, double sv, double a, double w, double err) {
+  const TNode T = tnode_setup(xx, v, sv, a, err);
+  return tnode_pdf_sv(T, w, v, sv, a);
+}
+
+// ---------------------------------------------------------------------------
+// Adaptive Simpson (integrate.pxi:72-141, 143-206) as an iterative walk.
+struct Frame {
+  double lb, ub, S, fb, fe, fm, err, left;
+};
+
+// Depth <= N frames held in registers: every access is a compile-time index
+// after unrolling, so the array is scalarised (no scratch).
+template <int N>
+struct RegStack {
+  static constexpr int kCap = N;
+  Frame f[N];
+  __device__ inline Frame get(int i) const {
+    Frame r = f[0];
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+      if (i == k) r = f[k];
+    return r;
+  }
+  __device__ inline double left(int i) const {
+    double r = f[0].left;
+#pragma unroll
+    for (int k = 1; k < N; ++k)
+      if (i == k) r = f[k].left;
+    return r;
+  }
+  __device__ inline void set(int i, const Frame& x) {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (i == k) f[k] = x;
+  }
+  __device__ inline void set_left(int i, double v) {
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+      if (i == k) f[k].left = v;
+  }
+};
+
+// Arbitrary depth (up to N): plain private array (scratch memory).
+template <int N>
+struct MemStack {
+  static constexpr int kCap = N;
+  Frame f[N];
+  __device__ inline Frame get(int i) const { return f[i]; }
+  __device__ inline double left(int i) const { return f[i].left; }
+  __device__ inline void set(int i, const Frame& x) { f[i] = x; }
+  __device__ inline void set_left(int i, double v) { f[i].left = v; }
+};
+
+// Integrates g over [lb0, ub0] exactly like adaptiveSimpsons_1D/_2D followed by
+// adaptiveSimpsonsAux(_2D): g(c) must already include the division by ZT (or st).
+// Every lane walks its own quadrature tree; each loop trip evaluates g at the 3
+// initial nodes or at the 2 new nodes of one interval, from ONE call site.
+// A refinement deeper than the stack capacity sets `overflow` (the call then
+// fails with WFPT_ERR_UNSUPPORTED instead of returning a wrong number).
+template <class Stack, class G>
+__device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double err0,
+                                          int depth, int& overflow) {
+  Stack stk;
+  double lb = lb0, ub = ub0, err = err0;
+  double S = 0.0, fb = 0.0, fe = 0.0, fm = 0.0;
+  int bottom = depth, sp = 0;
+  unsigned right_mask = 0u;  // bit i: frame i has finished its left child
+  bool init = true;
+  double result = 0.0;
+  for (;;) {
+    const double c = (ub + lb) / 2.;
+    const double p0 = init ? lb : (lb + c) / 2.;
+    const double p1 = init ? ub : (c + ub) / 2.;
+    const int n = init ? 3 : 2;
+    double y0 = 0.0, y1 = 0.0, y2 = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < n; ++i) {
+      const double p = (i == 0) ? p0 : ((i == 1) ? p1 : c);
+      const double y = g(p);
+      if (i == 0) y0 = y;
+      else if (i == 1) y1 = y;
+      else y2 = y;
+    }
+    const double h = ub - lb;
+    if (init) {  // adaptiveSimpsons_1D / _2D prologue
+      fb = y0;
+      fe = y1;
+      fm = y2;
+      S = (h / 6) * ((fb + (4 * fm)) + fe);
+      init = false;
+      continue;
+    }
+    // adaptiveSimpsonsAux body (integrate.pxi:105-112 / 170-178)
+    const double fd = y0, fee = y1;
+    const double Sl = (h / 12) * ((fb + (4 * fd)) + fm);
+    const double Sr = (h / 12) * ((fm + (4 * fee)) + fe);
+    const double S2 = Sl + Sr;
+    const bool refine = !(bottom <= 0 || fabs(S2 - S) <= 15 * err);
+    if (refine && sp >= Stack::kCap) overflow = 1;
+    if (refine && sp < Stack::kCap) {
+      Frame fr;
+      fr.lb = c;
+      fr.ub = ub;
+      fr.S = Sr;
+      fr.fb = fm;
+      fr.fe = fe;
+      fr.fm = fee;
+      fr.err = err / 2;
+      fr.left = 0.0;
+      stk.set(sp, fr);
+      ++sp;
+      ub = c;
+      err = err / 2;
+      S = Sl;
+      fe = fm;
+      fm = fd;
+      bottom -= 1;
+      continue;
+    }
+    double val = S2 + (S2 - S) / 15;
+    bool done = false;
+    for (;;) {  // return up the tree: left + right in reference order
+      if (sp == 0) {
+        result = val;
+        done = true;
+        break;
+      }
+      const int top = sp - 1;
+      if (!((right_mask >> top) & 1u)) {
+        const Frame fr = stk.get(top);
+        stk.set_left(top, val);
+        right_mask |= (1u << top);
+        lb = fr.lb;
+        ub = fr.ub;
+        S = fr.S;
+        fb = fr.fb;
+        fe = fr.fe;
+        fm = fr.fm;
+        err = fr.err;
+        bottom = depth - sp;
+        break;
+      }
+      val = stk.left(top) + val;
+      right_mask &= ~(1u << top);
+      --sp;
+    }
+    if (done) break;
+  }
+  return result;
+}
+
+// Fixed composite Simpson, integrate.pxi:12-45. Returns the integral; the
+// reference leaves `y` uninitialised when n == 0 (0 here).
+template <bool COUNT>
+__device__ inline double simpson_1d(double x, double v, double sv, double a, double z, double t,
+                                    double err, double lb_z, double ub_z, int n_sz, double lb_t,
+                                    double ub_t, int n_st, long long& ne) {
+  double ht, hz;
+  const int n = (n_st < n_sz) ? n_sz : n_st;
+  if (n_st == 0) {
+    hz = (ub_z - lb_z) / n;
+    ht = 0;
+    lb_t = t;
+    ub_t = t;
+  } else {
+    hz = 0;
+    ht = (ub_t - lb_t) / n;
+    lb_z = z;
+    ub_z = z;
+  }
+  if (COUNT) ++ne;
+  double S = pdf_sv(x - lb_t, v, sv, a, lb_z, err);
+  double y = 0.0;
+  for (int i = 1; i <= n; ++i) {
+    const double z_tag = lb_z + hz * i;
+    const double t_tag = lb_t + ht * i;
+    if (COUNT) ++ne;
+    y = pdf_sv(x - t_tag, v, sv, a, z_tag, err);
+    if (i & 1) S += (4 * y);
+    else S += (2 * y);
+  }
+  S = S - y;
+  S = S / ((ub_t - lb_t) + (ub_z - lb_z));
+  return ((ht + hz) * S) / 3;
+}
+
+template <bool COUNT>
+__device__ inline double simpson_2d(double x, double v, double sv, double a, double z, double t,
+                                    double err, double lb_z, double ub_z, int n_sz, double lb_t,
+                                    double ub_t, int n_st, long long& ne) {
+  const double ht = (ub_t - lb_t) / n_st;
+  double S = simpson_1d<COUNT>(x, v, sv, a, z, lb_t, err, lb_z, ub_z, n_sz, 0, 0, 0, ne);
+  double y = 0.0;
+  for (int i_t = 1; i_t <= n_st; ++i_t) {
+    const double t_tag = lb_t + ht * i_t;
+    y = simpson_1d<COUNT>(x, v, sv, a, z, t_tag, err, lb_z, ub_z, n_sz, 0, 0, 0, ne);
+    if (i_t & 1) S += (4 * y);
+    else S += (2 * y);
+  }
+  S = S - y;
+  S = S / (ub_t - lb_t);
+  return (ht * S) / 3;
+}
+
+// full_pdf (pdf.pxi:104-146) for one trial. MODE is the launch-uniform
+// integration family (kRuntime: decided per lane).
+template <int MODE, class Stack, bool COUNT>
+__device__ inline double full_pdf(double x, const Params& P, const Knobs& K, long long& ne,
+                                  int& ovf) {
+  const double a = P.a, sv = P.sv, t = P.t;
+  double v = P.v, z = P.z, st = P.st, sz = P.sz;
+  if ((z < 0) || (z > 1) || (a < 0) || (t < 0) || (st < 0) || (sv < 0) || (sz < 0) ||
+      (sz > 1) || ((fabs(x) - (t - st / 2.)) < 0) || (z + sz / 2. > 1) || (z - sz / 2. < 0) ||
+      (t - st / 2. < 0))
+    return 0.0;
+  if (x > 0) {
+    v = -v;
+    z = 1. - z;
+  }
+  x = fabs(x);
+  if (st < 1e-3) st = 0;
+  if (sz < 1e-3) sz = 0;
+  const int mode = (MODE == kRuntime) ? select_mode(sz, st, K.use_adaptive) : MODE;
+  const double err = K.err;
+
+  if (mode == kDirect) {
+    if (COUNT) ++ne;
+    return pdf_sv(x - t, v, sv, a, z, err);
+  }
+  if (mode == kAdaptZ) {
+    // adaptiveSimpsons_1D over z at fixed t: one t node for every evaluation
+    const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
+    const double ZT = ub_z - lb_z;
+    const TNode T = tnode_setup(x - t, v, sv, a, err);
+    auto g = [&](double zc) -> double {
+      if (COUNT) ++ne;
+      return tnode_pdf_sv(T, zc, v, sv, a) / ZT;
+    };
+    return adaptive_simpson<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, ovf);
+  }
+  if (mode == kAdaptT) {
+    const double lb_t = t - st / 2., ub_t = t + st / 2.;
+    const double ZT = ub_t - lb_t;
+    auto g = [&](double tc) -> double {
+      if (COUNT) ++ne;
+      return pdf_sv(x - tc, v, sv, a, z, err) / ZT;
+    };
+    return adaptive_simpson<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, ovf);
+  }
+  if (mode == kAdaptTZ) {
+    const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
+    const double lb_t = t - st / 2., ub_t = t + st / 2.;
+    const double ZT = ub_z - lb_z;
+    const double stw = ub_t - lb_t;  // `st` of adaptiveSimpsons_2D (integrate.pxi:187)
+    const double e1 = K.simps_err;
+    const int nsz = K.n_sz;
+    auto outer = [&](double tc) -> double {
+      const TNode T = tnode_setup(x - tc, v, sv, a, err);
+      auto inner = [&](double zc) -> double {
+        if (COUNT) ++ne;
+        return tnode_pdf_sv(T, zc, v, sv, a) / ZT;
+      };
+      return adaptive_simpson<Stack>(inner, lb_z, ub_z, e1, nsz, ovf) / stw;
+    };
+    return adaptive_simpson<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, ovf);
+  }
+  if (mode == kFixedT)
+    return simpson_1d<COUNT>(x, v, sv, a, z, t, err, z, z, 0, t - st / 2., t + st / 2., K.n_st,
+                             ne);
+  if (mode == kFixedZ)
+    return simpson_1d<COUNT>(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz, t, t, 0,
+                             ne);
+  return simpson_2d<COUNT>(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz,
+                           t - st / 2., t + st / 2., K.n_st, ne);
+}
+
+// P(hit upper boundary), pdf.pxi:67-72
+__device__ inline double prob_ub(double v, double a, double z) {
+  if (v == 0) return z;
+  return (exp(((-2.0 * a) * z) * v) - 1.0) / (exp((-2.0 * a) * v) - 1.0);
+}
+
+}  // namespace wfpt

@@ -1,0 +1,29 @@
+// wfpt_internal.h — launcher interface between the C ABI (wfpt_capi.cpp) and
+// the kernels (wfpt_kernels.hip). Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/wfpt_amd.h"
+
+namespace wfpt {
+struct Params;
+struct Knobs;
+
+int stack_kind(const Knobs& K);
+int64_t blocks_for(int64_t n);
+// out_kind: 0 = block {sum, zeros}; 1 = per-trial density (logp => log); 2 = per-trial log p
+void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
+                   double* out, int* zeros, unsigned long long* evals, int* status, int logp,
+                   hipStream_t s);
+void launch_finalize(const double* part, const int* zeros, int64_t nb, double* out,
+                     hipStream_t s);
+void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
+                  const Knobs& K, double* lp, unsigned long long* evals, int* status,
+                  hipStream_t s);
+void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
+                        hipStream_t s);
+void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
+                  const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
+                  hipStream_t s);
+}  // namespace wfpt

@@ -1,0 +1,362 @@
+// wfpt_kernels.hip — gfx950 kernels of the WFPT likelihood engine.
+//
+//   trial_kernel<MODE, STK, COUNT, OUT>   one trial per lane: full_pdf, the
+//       outlier mixture (wfpt.pyx:69-70) and either the per-block
+//       {sum log p, #zeros} (OUT_SUM, fused wave/LDS tree reduction) or the
+//       per-trial density / log density (OUT_ARRAY, pdf_array), or per-trial
+//       log p for the segmented per-node reduction (OUT_LOGP).
+//   finalize_kernel       deterministic second pass over block partials.
+//   segment_sum_kernel    per-node sums (one wave per node).
+//   multi_kernel          per-trial parameters (wiener_like_multi).
+// No float atomics on any likelihood value: every sum is a fixed-order tree.
+#include "wfpt_device.hpp"
+#include "wfpt_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace wfpt {
+
+constexpr int kBlock = 256;
+
+enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
+
+__device__ inline double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ inline long long wave_sum_ll(long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block (256 lanes = 4 waves) reduction of (sum, zeros, evals); lane 0 returns.
+template <bool COUNT>
+__device__ inline void block_reduce(double& s, int& zeros, long long& ne) {
+  __shared__ double ss[kBlock / 64];
+  __shared__ int sz[kBlock / 64];
+  __shared__ long long sn[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  s = wave_sum(s);
+  const unsigned long long zb = __ballot(zeros != 0);
+  if (COUNT) ne = wave_sum_ll(ne);
+  if (lane == 0) {
+    ss[w] = s;
+    sz[w] = __popcll(zb);
+    if (COUNT) sn[w] = ne;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s = ((ss[0] + ss[1]) + (ss[2] + ss[3]));
+    zeros = sz[0] + sz[1] + sz[2] + sz[3];
+    if (COUNT) ne = sn[0] + sn[1] + sn[2] + sn[3];
+  }
+}
+
+struct TrialArgs {
+  const double* x;
+  int64_t n;
+  Params P;
+  Knobs K;
+  double wp_outlier;      // w_outlier * p_outlier
+  double* out;            // OUT_SUM: block sums; OUT_ARRAY/OUT_LOGP: per trial
+  int* zeros;             // OUT_SUM: block zero counts
+  unsigned long long* evals;
+  int* status;            // set to 1 if a trial overflowed the Simpson stack
+  int logp;               // OUT_ARRAY: return log density
+};
+
+template <int STK>
+struct StackOf;
+template <>
+struct StackOf<0> {
+  using type = RegStack<2>;
+};
+template <>
+struct StackOf<1> {
+  using type = RegStack<4>;
+};
+template <>
+struct StackOf<2> {
+  using type = MemStack<WFPT_MAX_DEPTH>;
+};
+
+template <int MODE, int STK, bool COUNT, int OUT>
+__global__ __launch_bounds__(kBlock) void trial_kernel(TrialArgs A) {
+  using Stack = typename StackOf<STK>::type;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  long long ne = 0;
+  double lp = 0.0;
+  int zero = 0, ovf = 0;
+  if (i < A.n) {
+    double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
+    if (ovf) atomicOr(A.status, 1);
+    if (OUT == OUT_ARRAY) {
+      p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
+      A.out[i] = A.logp ? log(p) : p;
+    } else {
+      p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
+      if (p == 0) zero = 1;
+      else lp = log(p);
+      if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+    }
+  }
+  if (OUT == OUT_SUM || COUNT) {
+    block_reduce<COUNT>(lp, zero, ne);
+    if (threadIdx.x == 0) {
+      if (OUT == OUT_SUM) {
+        A.out[blockIdx.x] = lp;
+        A.zeros[blockIdx.x] = zero;
+      }
+      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
+    }
+  }
+}
+
+// out[0] = sum of partials, out[1] = number of zero trials (as double).
+__global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
+                                                        int64_t nb, double* out) {
+  __shared__ double ss[16];
+  __shared__ long long sz[16];
+  double s = 0.0;
+  long long z = 0;
+  for (int64_t b = threadIdx.x; b < nb; b += 1024) {
+    s += part[b];
+    z += zeros[b];
+  }
+  s = wave_sum(s);
+  z = wave_sum_ll(z);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    ss[w] = s;
+    sz[w] = z;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    long long zz = 0;
+    for (int k = 0; k < 16; ++k) {
+      t += ss[k];
+      zz += sz[k];
+    }
+    out[0] = t;
+    out[1] = (double)zz;
+  }
+}
+
+// One wave per node: sums per-trial log p of [off[j], off[j+1]) in fixed order.
+// out[j] = -inf if the node holds a zero-density trial (wfpt.pyx:71-72).
+__global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, const int64_t* off,
+                                                          int32_t n_nodes, double* out) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= n_nodes) return;
+  const int64_t lo = off[j], hi = off[j + 1];
+  double s = 0.0;
+  int zero = 0;
+  for (int64_t i = lo + lane; i < hi; i += 64) {
+    const double v = lp[i];
+    if (v == -INFINITY) zero = 1;
+    else s += v;
+  }
+  s = wave_sum(s);
+  const bool anyz = __ballot(zero != 0) != 0ull;
+  if (lane == 0) out[j] = anyz ? -INFINITY : s;
+}
+
+// Per-node parameters: trials of node j read P[j] (wfpt_wiener_like_nodes).
+template <int STK, bool COUNT>
+__global__ __launch_bounds__(kBlock) void node_kernel(const double* x, const int32_t* node,
+                                                      int64_t n, const Params* P, Knobs K,
+                                                      double* lp, unsigned long long* evals,
+                                                      int* status) {
+  using Stack = typename StackOf<STK>::type;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  long long ne = 0;
+  double out = 0.0;
+  int zero = 0, ovf = 0;
+  if (i < n) {
+    const Params Q = P[node[i]];
+    double p = full_pdf<kRuntime, Stack, COUNT>(x[i], Q, K, ne, ovf);
+    if (ovf) atomicOr(status, 1);
+    const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);
+    p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
+    if (!ok || p == 0) zero = 1;
+    else out = log(p);
+    lp[i] = zero ? -INFINITY : out;
+  }
+  if (COUNT) {
+    double d = 0.0;
+    block_reduce<COUNT>(d, zero, ne);
+    if (threadIdx.x == 0) atomicAdd(evals, (unsigned long long)ne);
+  }
+}
+
+// wiener_like_multi (wfpt.pyx:244-274): per-trial parameters, ±999 = missing.
+template <int STK>
+__global__ __launch_bounds__(kBlock) void multi_kernel(const double* x, int64_t n,
+                                                       const double* const* arr,
+                                                       const double* scal, Knobs K,
+                                                       double p_outlier, double* out,
+                                                       int* zeros, int* status) {
+  using Stack = typename StackOf<STK>::type;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double lp = 0.0;
+  int zero = 0, ovf = 0;
+  long long ne = 0;
+  if (i < n) {
+    double q[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) q[j] = arr[j] ? arr[j][i] : scal[j];
+    Params Q;
+    Q.v = q[0];
+    Q.sv = q[1];
+    Q.a = q[2];
+    Q.z = q[3];
+    Q.sz = q[4];
+    Q.t = q[5];
+    Q.st = q[6];
+    Q.p_outlier = p_outlier;
+    const double xi = x[i];
+    double p;
+    if (fabs(xi) != 999.) {
+      p = full_pdf<kRuntime, Stack, false>(xi, Q, K, ne, ovf);
+      if (ovf) atomicOr(status, 1);
+      p = p * (1 - p_outlier) + (K.w_outlier * p_outlier);
+    } else if (xi == 999.) {
+      p = prob_ub(Q.v, Q.a, Q.z);
+    } else {
+      p = 1 - prob_ub(Q.v, Q.a, Q.z);
+    }
+    // the reference has no early exit here: log(0) = -inf enters the sum
+    lp = log(p);
+  }
+  block_reduce<false>(lp, zero, ne);
+  if (threadIdx.x == 0) {
+    out[blockIdx.x] = lp;
+    zeros[blockIdx.x] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+
+template <int MODE, int STK, bool COUNT>
+static void launch_mode(int out_kind, const TrialArgs& A, int64_t nb, hipStream_t s) {
+  switch (out_kind) {
+    case OUT_SUM:
+      hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT_SUM>), dim3(nb), dim3(kBlock), 0, s,
+                         A);
+      break;
+    case OUT_ARRAY:
+      hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT_ARRAY>), dim3(nb), dim3(kBlock), 0,
+                         s, A);
+      break;
+    default:
+      hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT_LOGP>), dim3(nb), dim3(kBlock), 0,
+                         s, A);
+      break;
+  }
+}
+
+template <int MODE, bool COUNT>
+static void launch_stk(int stk, int out_kind, const TrialArgs& A, int64_t nb, hipStream_t s) {
+  if (stk == 0) launch_mode<MODE, 0, COUNT>(out_kind, A, nb, s);
+  else if (stk == 1) launch_mode<MODE, 1, COUNT>(out_kind, A, nb, s);
+  else launch_mode<MODE, 2, COUNT>(out_kind, A, nb, s);
+}
+
+template <bool COUNT>
+static void launch_all(int mode, int stk, int out_kind, const TrialArgs& A, int64_t nb,
+                       hipStream_t s) {
+  switch (mode) {
+    case kDirect: launch_mode<kDirect, 0, COUNT>(out_kind, A, nb, s); break;
+    case kAdaptT: launch_stk<kAdaptT, COUNT>(stk, out_kind, A, nb, s); break;
+    case kAdaptZ: launch_stk<kAdaptZ, COUNT>(stk, out_kind, A, nb, s); break;
+    case kAdaptTZ: launch_stk<kAdaptTZ, COUNT>(stk, out_kind, A, nb, s); break;
+    case kFixedT: launch_mode<kFixedT, 0, COUNT>(out_kind, A, nb, s); break;
+    case kFixedZ: launch_mode<kFixedZ, 0, COUNT>(out_kind, A, nb, s); break;
+    default: launch_mode<kFixedTZ, 0, COUNT>(out_kind, A, nb, s); break;
+  }
+}
+
+int stack_kind(const Knobs& K) {
+  const int d = (K.n_st > K.n_sz) ? K.n_st : K.n_sz;
+  return d <= 2 ? 0 : (d <= 4 ? 1 : 2);
+}
+
+int64_t blocks_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
+
+void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
+                   double* out, int* zeros, unsigned long long* evals, int* status, int logp,
+                   hipStream_t s) {
+  TrialArgs A;
+  A.x = x;
+  A.n = n;
+  A.P = P;
+  A.K = K;
+  A.wp_outlier = K.w_outlier * P.p_outlier;
+  A.out = out;
+  A.zeros = zeros;
+  A.evals = evals;
+  A.status = status;
+  A.logp = logp;
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  const int64_t nb = blocks_for(n);
+  if (nb == 0) return;
+  if (evals) launch_all<true>(mode, stack_kind(K), out_kind, A, nb, s);
+  else launch_all<false>(mode, stack_kind(K), out_kind, A, nb, s);
+}
+
+void launch_finalize(const double* part, const int* zeros, int64_t nb, double* out,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, out);
+}
+
+void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
+                  const Knobs& K, double* lp, unsigned long long* evals, int* status,
+                  hipStream_t s) {
+  const int64_t nb = blocks_for(n);
+  if (nb == 0) return;
+  const int stk = stack_kind(K);
+#define NODE_LAUNCH(S_, C_)                                                                  \
+  hipLaunchKernelGGL((node_kernel<S_, C_>), dim3(nb), dim3(kBlock), 0, s, x, node, n, P, K, \
+                     lp, evals, status)
+  if (evals) {
+    if (stk == 0) NODE_LAUNCH(0, true);
+    else if (stk == 1) NODE_LAUNCH(1, true);
+    else NODE_LAUNCH(2, true);
+  } else {
+    if (stk == 0) NODE_LAUNCH(0, false);
+    else if (stk == 1) NODE_LAUNCH(1, false);
+    else NODE_LAUNCH(2, false);
+  }
+#undef NODE_LAUNCH
+}
+
+void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
+                        hipStream_t s) {
+  if (n_nodes <= 0) return;
+  hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
+                     n_nodes, out);
+}
+
+void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
+                  const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
+                  hipStream_t s) {
+  const int64_t nb = blocks_for(n);
+  if (nb == 0) return;
+  const int stk = stack_kind(K);
+  if (stk == 0)
+    hipLaunchKernelGGL((multi_kernel<0>), dim3(nb), dim3(kBlock), 0, s, x, n, arr, scal, K,
+                       p_outlier, part, zeros, status);
+  else if (stk == 1)
+    hipLaunchKernelGGL((multi_kernel<1>), dim3(nb), dim3(kBlock), 0, s, x, n, arr, scal, K,
+                       p_outlier, part, zeros, status);
+  else
+    hipLaunchKernelGGL((multi_kernel<2>), dim3(nb), dim3(kBlock), 0, s, x, n, arr, scal, K,
+                       p_outlier, part, zeros, status);
+}
+
+}  // namespace wfpt

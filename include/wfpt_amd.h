@@ -1,0 +1,133 @@
+/*
+ * wfpt_amd — MI355X (gfx950) Wiener first-passage-time likelihood engine.
+ *
+ * C ABI that replaces the reference's `wfpt` Cython extension module on its
+ * hot path. Plain pointers and sizes only; device memory, streams and RCCL
+ * communicators live behind opaque handles. Every entry point returns a
+ * status (WFPT_OK == 0); a non-zero status is a device / argument error and is
+ * never folded into a numeric result. Numeric failure keeps the reference's
+ * conventions exactly: -inf for an impossible likelihood, 0 for an invalid
+ * parameter set per trial, NaN where the reference yields NaN (a == 0).
+ *
+ * Reference interfaces replaced (file:line under the reference tree):
+ *   wfpt_wiener_like*      <- wfpt.wiener_like         src/wfpt.pyx:54-76
+ *   wfpt_pdf_array         <- wfpt.pdf_array           src/wfpt.pyx:32-48
+ *   wfpt_full_pdf          <- wfpt.full_pdf (cpdef)    src/pdf.pxi:104-146
+ *   wfpt_wiener_like_nodes <- one wfpt_like per PyMC node, batched
+ *                             hddm/likelihoods.py:52-73 via base.py:754-757
+ *   wfpt_wiener_like_multi <- wfpt.wiener_like_multi   src/wfpt.pyx:244-274
+ * The Python binding that keeps the reference signatures is
+ * hddm_amd/wfpt.py (ctypes); INTEGRATION.md shows the drop-in.
+ */
+#ifndef WFPT_AMD_H
+#define WFPT_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WFPT_OK 0
+#define WFPT_ERR_HIP 1         /* HIP runtime / kernel failure */
+#define WFPT_ERR_ARG 2         /* bad argument (null pointer, size, depth) */
+#define WFPT_ERR_COMM 3        /* RCCL failure */
+#define WFPT_ERR_UNSUPPORTED 4 /* e.g. n_st/n_sz beyond WFPT_MAX_DEPTH */
+
+/* Maximum adaptive-Simpson recursion depth (n_st, n_sz) supported on device.
+ * The reference recurses without bound; 2^24 leaves per trial is far past any
+ * practical use (HDDM passes 2, wiener_like's default is 10). */
+#define WFPT_MAX_DEPTH 24
+
+typedef struct wfpt_ctx wfpt_ctx;
+typedef struct wfpt_ds wfpt_ds;
+
+/* DDM parameters of one likelihood call (src/wfpt.pyx:54: v sv a z sz t st
+ * p_outlier). */
+typedef struct wfpt_params {
+    double v, sv, a, z, sz, t, st, p_outlier;
+} wfpt_params;
+
+/* Numerical knobs (src/wfpt.pyx:55-56). All explicit: the reference's own
+ * defaults differ between wiener_like and pdf_array. */
+typedef struct wfpt_knobs {
+    double err;           /* series truncation error (pdf.pxi:36-47) */
+    int32_t n_st;         /* max recursion depth over st */
+    int32_t n_sz;         /* max recursion depth over sz */
+    int32_t use_adaptive; /* 0 => fixed Simpson with n_st/n_sz panels */
+    double simps_err;     /* adaptive Simpson tolerance */
+    double w_outlier;     /* outlier density */
+} wfpt_knobs;
+
+/* ---- context ---------------------------------------------------------- */
+int wfpt_device_count(int *n);
+int wfpt_open(int device, wfpt_ctx **out);
+void wfpt_close(wfpt_ctx *ctx);
+/* message of the last failing call on this thread ("" if none) */
+const char *wfpt_last_error(void);
+
+/* ---- resident datasets ------------------------------------------------- */
+/* Uploads rt[n] (signed RTs, sign = boundary, hddm/utils.py:15-37) once.
+ * node_id (nullable) assigns each trial to one of n_nodes likelihood nodes
+ * (hierarchical models); trials are regrouped by node and, inside a node,
+ * ordered by |rt| so one wavefront sees one series branch.
+ * The caller's arrays are not retained. */
+int wfpt_dataset_create(wfpt_ctx *ctx, const double *rt, int64_t n, const int32_t *node_id,
+                        int32_t n_nodes, wfpt_ds **out);
+void wfpt_dataset_destroy(wfpt_ds *ds);
+int64_t wfpt_dataset_size(const wfpt_ds *ds);
+/* The i-th rank's contiguous shard [lo, hi) of n trials (multi-GPU). */
+void wfpt_shard_range(int64_t n, int nranks, int rank, int64_t *lo, int64_t *hi);
+
+/* ---- likelihoods -------------------------------------------------------- */
+/* Sum of log mixture densities over a resident dataset (wfpt.pyx:54-76). */
+int wfpt_wiener_like(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
+                     const wfpt_knobs *k, double *out_logp);
+/* Same on a host array (uploaded for this call). */
+int wfpt_wiener_like_host(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
+                          const wfpt_knobs *k, double *out_logp);
+/* Per-node sums for a dataset created with node ids: params[n_nodes] in,
+ * out_logp[n_nodes] out (each = wiener_like of that node's trials). */
+int wfpt_wiener_like_nodes(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *per_node,
+                           const wfpt_knobs *k, double *out_logp);
+/* Per-trial mixture density, or its log if logp != 0 (wfpt.pyx:32-48). */
+int wfpt_pdf_array(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
+                   const wfpt_knobs *k, int logp, double *out);
+/* Single full_pdf (no mixture) (pdf.pxi:104-146). */
+int wfpt_full_pdf(wfpt_ctx *ctx, double x, const wfpt_params *p, const wfpt_knobs *k,
+                  double *out);
+/* Per-trial parameters (wfpt.pyx:244-274). arrays[j] (j = v,sv,a,z,sz,t,st)
+ * is a host array of n values or NULL to use scalars[j]. |x| == 999 marks a
+ * missing response scored by prob_ub (pdf.pxi:67-72). */
+int wfpt_wiener_like_multi(wfpt_ctx *ctx, const double *x, int64_t n,
+                           const double *const arrays[7], const double scalars[7],
+                           const wfpt_knobs *k, double p_outlier, double *out_logp);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) -------------------- */
+/* 128-byte RCCL unique id, created on rank 0 and broadcast by the caller. */
+int wfpt_comm_unique_id(unsigned char id[128]);
+int wfpt_comm_init(wfpt_ctx *ctx, int nranks, int rank, const unsigned char id[128]);
+/* wiener_like over this rank's resident shard, combined across ranks with one
+ * ncclAllReduce of {sum log p, #zero trials} (2 doubles); every rank receives
+ * the global total. */
+int wfpt_wiener_like_allreduce(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
+                               const wfpt_knobs *k, double *out_logp);
+
+/* ---- measurement -------------------------------------------------------- */
+/* flags & WFPT_PROF_EVENTS: bracket the main likelihood kernel of each call
+ * with HIP events on the context's stream (per-launch device time);
+ * flags & WFPT_PROF_EVALS: count pdf_sv evaluations (a separate kernel build
+ * with one integer atomic per block; use it in an untimed pass). 0 = off. */
+#define WFPT_PROF_EVENTS 1
+#define WFPT_PROF_EVALS 2
+int wfpt_profile_enable(wfpt_ctx *ctx, int flags);
+/* Accumulated main-kernel milliseconds, launches and pdf_sv evaluations since
+ * the last reset. */
+int wfpt_profile_read(wfpt_ctx *ctx, double *kernel_ms, int64_t *launches, int64_t *n_evals,
+                      int reset);
+int wfpt_synchronize(wfpt_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WFPT_AMD_H */

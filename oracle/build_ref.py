@@ -1,0 +1,49 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+Recipe that compiles the reference's own WFPT kernels (src/pdf.pxi +
+src/integrate.pxi, read where they lie under /root/reference) into
+oracle/_ref/ref_shim<EXT_SUFFIX>. Outputs go only into oracle/_ref/ (git-ignored).
+
+Mirrors the reference build of setup.py:4-7 (Cython -> C++, g++ -O2, no
+-fopenmp). Cython's `include "integrate.pxi"` is resolved through the
+include path, so nothing from the reference is copied into this repository.
+
+Usage:  python oracle/build_ref.py [--reference /root/reference]
+"""
+import argparse
+import os
+import subprocess
+import sys
+import sysconfig
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+OUT = os.path.join(HERE, "_ref")
+
+
+def build(reference="/root/reference", quiet=False):
+    src = os.path.join(reference, "src")
+    if not os.path.isfile(os.path.join(src, "integrate.pxi")):
+        raise FileNotFoundError(f"reference sources not found under {src}")
+    import numpy as np
+    os.makedirs(OUT, exist_ok=True)
+    cpp = os.path.join(OUT, "ref_shim.cpp")
+    so = os.path.join(OUT, "ref_shim" + sysconfig.get_config_var("EXT_SUFFIX"))
+    pyx = os.path.join(HERE, "ref_shim.pyx")
+    if (os.path.exists(so) and os.path.getmtime(so) > os.path.getmtime(pyx)
+            and os.path.getmtime(so) > os.path.getmtime(os.path.join(src, "integrate.pxi"))
+            and os.path.getmtime(so) > os.path.getmtime(os.path.join(src, "pdf.pxi"))):
+        return so
+    run = (lambda c: subprocess.run(c, check=True, stdout=subprocess.DEVNULL)) if quiet else \
+        (lambda c: subprocess.run(c, check=True))
+    run([sys.executable, "-m", "cython", "--cplus", "-2", "-I", src, "-o", cpp, pyx])
+    run(["g++", "-O2", "-fwrapv", "-fPIC", "-DNDEBUG", "-shared",
+         "-DNPY_NO_DEPRECATED_API=NPY_1_7_API_VERSION",
+         "-I", sysconfig.get_paths()["include"], "-I", np.get_include(),
+         cpp, "-o", so])
+    return so
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    print(build(ap.parse_args().reference))
