@@ -162,10 +162,14 @@ int fetch_status(wfpt_ctx* c) {
   return WFPT_OK;
 }
 int check_status(wfpt_ctx* c) {
-  if (*c->host_status)
+  const int st = *c->host_status;
+  if (st & 1)
     return fail(WFPT_ERR_UNSUPPORTED,
                 "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
                     std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)");
+  if (st & 2)
+    return fail(WFPT_ERR_UNSUPPORTED,
+                "a trial exceeded WFPT_EVAL_BUDGET pdf_sv evaluations (raise simps_err)");
   return WFPT_OK;
 }
 

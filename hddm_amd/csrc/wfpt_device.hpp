@@ -208,11 +208,15 @@ struct MemStack {
 // adaptiveSimpsonsAux(_2D): g(c) must already include the division by ZT (or st).
 // Every lane walks its own quadrature tree; each loop trip evaluates g at the 3
 // initial nodes or at the 2 new nodes of one interval, from ONE call site.
-// A refinement deeper than the stack capacity sets `overflow` (the call then
-// fails with WFPT_ERR_UNSUPPORTED instead of returning a wrong number).
+// A refinement deeper than the stack capacity (overflow |= 1) or a trial
+// exceeding kEvalBudget pdf_sv evaluations (overflow |= 2) abandons the trial
+// at once: the call then fails with WFPT_ERR_UNSUPPORTED instead of returning
+// a number, and no input can keep a wave busy without bound.
+constexpr long long kEvalBudget = 1ll << 24;
+
 template <class Stack, class G>
 __device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double err0,
-                                          int depth, int& overflow) {
+                                          int depth, int& overflow, const long long& ne) {
   Stack stk;
   double lb = lb0, ub = ub0, err = err0;
   double S = 0.0, fb = 0.0, fe = 0.0, fm = 0.0;
@@ -234,6 +238,11 @@ __device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double 
       else if (i == 1) y1 = y;
       else y2 = y;
     }
+    if (ne > kEvalBudget) overflow |= 2;
+    if (overflow) {
+      result = __builtin_nan("");
+      break;
+    }
     const double h = ub - lb;
     if (init) {  // adaptiveSimpsons_1D / _2D prologue
       fb = y0;
@@ -249,8 +258,12 @@ __device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double 
     const double Sr = (h / 12) * ((fm + (4 * fee)) + fe);
     const double S2 = Sl + Sr;
     const bool refine = !(bottom <= 0 || fabs(S2 - S) <= 15 * err);
-    if (refine && sp >= Stack::kCap) overflow = 1;
-    if (refine && sp < Stack::kCap) {
+    if (refine && sp >= Stack::kCap) {
+      overflow |= 1;
+      result = __builtin_nan("");
+      break;
+    }
+    if (refine) {
       Frame fr;
       fr.lb = c;
       fr.ub = ub;
@@ -321,13 +334,13 @@ __device__ inline double simpson_1d(double x, double v, double sv, double a, dou
     lb_z = z;
     ub_z = z;
   }
-  if (COUNT) ++ne;
+  ++ne;
   double S = pdf_sv(x - lb_t, v, sv, a, lb_z, err);
   double y = 0.0;
   for (int i = 1; i <= n; ++i) {
     const double z_tag = lb_z + hz * i;
     const double t_tag = lb_t + ht * i;
-    if (COUNT) ++ne;
+    ++ne;
     y = pdf_sv(x - t_tag, v, sv, a, z_tag, err);
     if (i & 1) S += (4 * y);
     else S += (2 * y);
@@ -377,7 +390,7 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
   const double err = K.err;
 
   if (mode == kDirect) {
-    if (COUNT) ++ne;
+    ++ne;
     return pdf_sv(x - t, v, sv, a, z, err);
   }
   if (mode == kAdaptZ) {
@@ -386,19 +399,19 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
     const double ZT = ub_z - lb_z;
     const TNode T = tnode_setup(x - t, v, sv, a, err);
     auto g = [&](double zc) -> double {
-      if (COUNT) ++ne;
+      ++ne;
       return tnode_pdf_sv(T, zc, v, sv, a) / ZT;
     };
-    return adaptive_simpson<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, ovf);
+    return adaptive_simpson<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, ovf, ne);
   }
   if (mode == kAdaptT) {
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
     const double ZT = ub_t - lb_t;
     auto g = [&](double tc) -> double {
-      if (COUNT) ++ne;
+      ++ne;
       return pdf_sv(x - tc, v, sv, a, z, err) / ZT;
     };
-    return adaptive_simpson<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, ovf);
+    return adaptive_simpson<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, ovf, ne);
   }
   if (mode == kAdaptTZ) {
     const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
@@ -410,12 +423,12 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
     auto outer = [&](double tc) -> double {
       const TNode T = tnode_setup(x - tc, v, sv, a, err);
       auto inner = [&](double zc) -> double {
-        if (COUNT) ++ne;
+        ++ne;
         return tnode_pdf_sv(T, zc, v, sv, a) / ZT;
       };
-      return adaptive_simpson<Stack>(inner, lb_z, ub_z, e1, nsz, ovf) / stw;
+      return adaptive_simpson<Stack>(inner, lb_z, ub_z, e1, nsz, ovf, ne) / stw;
     };
-    return adaptive_simpson<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, ovf);
+    return adaptive_simpson<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, ovf, ne);
   }
   if (mode == kFixedT)
     return simpson_1d<COUNT>(x, v, sv, a, z, t, err, z, z, 0, t - st / 2., t + st / 2., K.n_st,

@@ -91,7 +91,7 @@ __global__ __launch_bounds__(kBlock) void trial_kernel(TrialArgs A) {
   int zero = 0, ovf = 0;
   if (i < A.n) {
     double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
-    if (ovf) atomicOr(A.status, 1);
+    if (ovf) atomicOr(A.status, ovf);
     if (OUT == OUT_ARRAY) {
       p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
       A.out[i] = A.logp ? log(p) : p;
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void node_kernel(const double* x, const int
   if (i < n) {
     const Params Q = P[node[i]];
     double p = full_pdf<kRuntime, Stack, COUNT>(x[i], Q, K, ne, ovf);
-    if (ovf) atomicOr(status, 1);
+    if (ovf) atomicOr(status, ovf);
     const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);
     p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
     if (!ok || p == 0) zero = 1;
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void multi_kernel(const double* x, int64_t 
     double p;
     if (fabs(xi) != 999.) {
       p = full_pdf<kRuntime, Stack, false>(xi, Q, K, ne, ovf);
-      if (ovf) atomicOr(status, 1);
+      if (ovf) atomicOr(status, ovf);
       p = p * (1 - p_outlier) + (K.w_outlier * p_outlier);
     } else if (xi == 999.) {
       p = prob_ub(Q.v, Q.a, Q.z);

@@ -38,6 +38,11 @@ extern "C" {
  * The reference recurses without bound; 2^24 leaves per trial is far past any
  * practical use (HDDM passes 2, wiener_like's default is 10). */
 #define WFPT_MAX_DEPTH 24
+/* Per-trial cap on pdf_sv evaluations (2^24). The heaviest call in the
+ * reference's own tests needs 1.2e5 (wiener_like defaults n=10,
+ * simps_err=1e-8). Exceeding either limit fails the call with
+ * WFPT_ERR_UNSUPPORTED; no value is returned. */
+#define WFPT_EVAL_BUDGET (1ll << 24)
 
 typedef struct wfpt_ctx wfpt_ctx;
 typedef struct wfpt_ds wfpt_ds;

@@ -186,10 +186,16 @@ def test_edge_semantics(gpu):
 
 def test_depth_overflow_fails_loudly(gpu):
     x = np.array([0.35, 0.9, -1.3])
-    # a tolerance no adaptive scheme reaches forces refinement to the stack limit
+    # simps_err=0 refines every interval: the leftmost path hits the stack cap
+    # at once and the call must fail, not hang and not return a number.
+    with pytest.raises(NotImplementedError):
+        gpu.wiener_like(x, 0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.0, 1e-10, n_st=40, n_sz=40,
+                        simps_err=0.0)
     with pytest.raises(NotImplementedError):
         gpu.wiener_like(x, 0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-10, n_st=40, n_sz=40,
                         simps_err=0.0)
+    # legal but heavy: the reference's own test_pdf_integrate_to_one knobs
+    assert np.isfinite(gpu.wiener_like(x, 0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-8))
 
 
 def test_dataset_order_invariance_and_additivity(gpu, oracle_lib):
