@@ -31,29 +31,34 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, defines=(), out=None):
+    """Compile libwfpt_amd.so. `defines` (e.g. ["WFPT_FAST_WAVES=3"]) and `out`
+    build experiment variants next to the default library."""
     os.makedirs(LIBDIR, exist_ok=True)
+    lib = out or LIB
     deps = [os.path.join(CSRC, f) for f in DEPS] + [os.path.join(ROOT, "include", "wfpt_amd.h")]
-    if not force and not _stale(LIB, deps):
-        return LIB
+    if not force and not _stale(lib, deps):
+        return lib
     objs = []
+    tag = os.path.splitext(os.path.basename(lib))[0]
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, os.path.splitext(src)[0] + ".o")
-        cmd = [HIPCC, *CFLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(LIBDIR, tag + "_" + os.path.splitext(src)[0] + ".o")
+        cmd = [HIPCC, *CFLAGS, *[f"-D{d}" for d in defines], "-c", os.path.join(CSRC, src),
+               "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
            "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

@@ -75,6 +75,8 @@ struct wfpt_ctx {
   DevBuf<double> marr;    // wiener_like_multi parameter arrays
   DevBuf<double*> mptr;
   DevBuf<double> mscal;
+  DevBuf<unsigned char> wl;  // fast-pass worklists (lane ids per block)
+  DevBuf<int> wl_n;          // deferred trials per block
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
@@ -173,17 +175,25 @@ int check_status(wfpt_ctx* c) {
   return WFPT_OK;
 }
 
+int reserve_worklist(wfpt_ctx* c, int64_t n) {
+  const int64_t nb = wfpt::blocks_for(n);
+  HIP_TRY(c->wl.reserve(std::max<int64_t>(nb * 256, 1)));
+  HIP_TRY(c->wl_n.reserve(std::max<int64_t>(nb, 1)));
+  return WFPT_OK;
+}
+
 int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
             const wfpt::Knobs& K) {
-  const int64_t nb = wfpt::blocks_for(n);
+  const int64_t nb = wfpt::partials_for(n, P, K);
   if (int rc = begin_status(c)) return rc;
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->res.reserve(2));
+  if (int rc = reserve_worklist(c, n)) return rc;
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   wfpt::launch_trials(0, dx, n, P, K, c->part.p, c->zero.p, c->count ? c->evals : nullptr,
-                      c->status, 0, c->stream);
+                      c->status, 0, c->wl.p, c->wl_n.p, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   if (nb > 0) {
@@ -282,6 +292,8 @@ void wfpt_close(wfpt_ctx* c) {
   c->marr.release();
   c->mptr.release();
   c->mscal.release();
+  c->wl.release();
+  c->wl_n.release();
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -415,8 +427,9 @@ int wfpt_pdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p
   if (int rc = upload(c, x, n)) return rc;
   HIP_TRY(c->lp.reserve(n));
   if (int rc = begin_status(c)) return rc;
+  if (int rc = reserve_worklist(c, n)) return rc;
   wfpt::launch_trials(1, c->x.p, n, P, K, c->lp.p, nullptr, nullptr, c->status, logp == 1,
-                      c->stream);
+                      c->wl.p, c->wl_n.p, c->stream);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   if (int rc = fetch_status(c)) return rc;

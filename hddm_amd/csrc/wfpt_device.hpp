@@ -57,12 +57,36 @@ __host__ __device__ inline int select_mode(double sz, double st, int use_adaptiv
 
 // ---------------------------------------------------------------------------
 // Per-t-node quantities of ftt_01w / pdf_sv that do not depend on w (= z).
+//
+// Decisions (pos, small/large branch, K) are computed with the reference's
+// exact operations. Values use cheaper equivalent forms whose rounding differs
+// by a few ulp (WFPT_EXACT_MATH=1 restores the literal expression order):
+//   * exp(-k^2 pi^2 tt/2) = q^(k^2), q = exp(-pi^2 tt/2), by two products per k;
+//   * sin(k pi w) by the Chebyshev recurrence from one sincospi(w);
+//   * exp(log p + c) = p * exp(c)  (overflow of exp(c) falls back to the
+//     literal form; p < 0 keeps the reference's NaN from log);
+//   * divisions by per-node constants become multiplications by reciprocals.
+#ifndef WFPT_EXACT_MATH
+#define WFPT_EXACT_MATH 0
+#endif
+// WFPT_SUBNORMAL_GUARD=1: where a value enters the subnormal range, take the
+// literal reference expression (one subnormal ulp can be a 1e-5 relative
+// change of a density below DBL_MIN). Off by default: such densities are
+// compared on the subnormal grid (|dp| <= 8 ulps), see tests/test_gpu_parity.py.
+#ifndef WFPT_SUBNORMAL_GUARD
+#define WFPT_SUBNORMAL_GUARD 0
+#endif
+constexpr double kDblMin = 2.2250738585072014e-308;
+constexpr double kSubnormalLo = -745.2, kSubnormalHi = -708.3;  // exp() subnormal band
+
 struct TNode {
   double xx;    // x - t_node: the `x` argument of pdf_sv
   double tt;    // xx / a^2 (pdf.pxi:98)
-  double norm;  // small-t: sqrt(2*pi*tt^3) divisor (pdf.pxi:57)
-  double den;   // sv: 2*sv^2*xx + 2   (pdf.pxi:102)
-  double sq;    // sv: sqrt(sv^2*xx + 1)
+  double m;     // small-t: -1/(2 tt) exponent multiplier; large-t: q = exp(-pi^2 tt / 2)
+  double q2;    // large-t: q^2
+  double rn;    // small-t: 1 / sqrt(2 pi tt^3)  (pdf.pxi:57)
+  double sc;    // 1/a^2, times 1/sqrt(sv^2 xx + 1) when sv > 0
+  double cden;  // sv: 1 / (2 sv^2 xx + 2)
   double vvx;   // v^2 * xx
   int K;        // number of series terms (pdf.pxi:52, 60)
   int small;    // 1 => small-time series
@@ -74,14 +98,17 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   T.xx = xx;
   T.pos = xx > 0;
   T.tt = 0.0;
-  T.norm = 1.0;
-  T.den = 1.0;
-  T.sq = 1.0;
+  T.m = 0.0;
+  T.q2 = 0.0;
+  T.rn = 0.0;
+  T.sc = 0.0;
+  T.cden = 0.0;
   T.vvx = 0.0;
   T.K = 0;
   T.small = 0;
   if (!T.pos) return T;
-  const double tt = xx / (a * a);
+  const double a2 = a * a;
+  const double tt = xx / a2;
   T.tt = tt;
   double kl, ks;
   // pdf.pxi:36-40
@@ -104,14 +131,18 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   if (ks < kl) {
     T.small = 1;
     T.K = (int)ceil(ks);
-    T.norm = sqrt((2.0 * kPi) * pow(tt, 3.0));
+    T.rn = 1.0 / sqrt((2.0 * kPi) * pow(tt, 3.0));
+    T.m = -0.5 / tt;
   } else {
     T.small = 0;
     T.K = (int)ceil(kl);
+    T.m = exp((-kPi2 * tt) / 2.0);
+    T.q2 = T.m * T.m;
   }
+  T.sc = 1.0 / a2;
   if (sv != 0) {
-    T.den = ((2.0 * (sv * sv)) * xx) + 2.0;
-    T.sq = sqrt(((sv * sv) * xx) + 1.0);
+    T.cden = 1.0 / (((2.0 * (sv * sv)) * xx) + 2.0);
+    T.sc = T.sc / sqrt(((sv * sv) * xx) + 1.0);
   }
   T.vvx = (v * v) * xx;
   return T;
@@ -120,21 +151,48 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
 // f(t|0,1,w) from a prepared t node (pdf.pxi:49-65).
 __device__ inline double tnode_ftt(const TNode& T, double w) {
   double p = 0.0;
+  const int K = T.K;
   if (T.small) {
-    const int K = T.K;
     const int lower = (int)(-floor((K - 1) / 2.));
     const int upper = (int)ceil((K - 1) / 2.);
     for (int k = lower; k <= upper; ++k) {
       const double wk = w + (double)(2 * k);
+#if WFPT_EXACT_MATH
       p = p + wk * exp(((-(wk * wk)) / 2.0) / T.tt);
+#else
+      double arg = (wk * wk) * T.m;
+      if (WFPT_SUBNORMAL_GUARD && arg < kSubnormalHi && arg > kSubnormalLo)
+        arg = ((-(wk * wk)) / 2.0) / T.tt;  // subnormal term: the reference's rounding
+      p = p + wk * exp(arg);
+#endif
     }
-    p = p / T.norm;
+#if WFPT_EXACT_MATH
+    p = p / sqrt((2.0 * kPi) * pow(T.tt, 3.0));
+#else
+    p = p * T.rn;
+#endif
   } else {
-    const int K = T.K;
+#if WFPT_EXACT_MATH
     for (int k = 1; k <= K; ++k) {
       const double dk = (double)k;
       p = p + (dk * exp((((-(dk * dk)) * kPi2) * T.tt) / 2.0)) * sin((dk * kPi) * w);
     }
+#else
+    double s1, c1;
+    sincospi(w, &s1, &c1);
+    const double tc = c1 + c1;
+    double sk = s1, skm1 = 0.0;          // sin(k pi w), sin((k-1) pi w)
+    double e = T.m, r = T.m * T.q2;      // q^(k^2), q^(2k+1)
+    if (K >= 1) p = e * s1;
+    for (int k = 2; k <= K; ++k) {
+      const double sn = tc * sk - skm1;
+      skm1 = sk;
+      sk = sn;
+      e = e * r;
+      r = r * T.q2;
+      p = p + ((double)k * e) * sk;
+    }
+#endif
     p = p * kPi;
   }
   return p;
@@ -144,10 +202,32 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
 __device__ inline double tnode_pdf_sv(const TNode& T, double w, double v, double sv, double a) {
   if (!T.pos) return 0.0;
   const double p = tnode_ftt(T, w);
+#if WFPT_EXACT_MATH
   if (sv == 0) return (p * exp((((-v) * a) * w) - (T.vvx / 2.))) / (a * a);
   const double azsv = (a * w) * sv;
-  return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) / T.den) / T.sq) /
+  return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) /
+                          (((2.0 * (sv * sv)) * T.xx) + 2.0)) /
+          sqrt(((sv * sv) * T.xx) + 1.0)) /
          (a * a);
+#else
+  if (sv == 0) {
+    const double ex = exp((((-v) * a) * w) - (T.vvx * 0.5));
+    const double r = (p * ex) * T.sc;
+    if (WFPT_SUBNORMAL_GUARD && fabs(r) < kDblMin && r != 0) return (p * ex) / (a * a);
+    return r;
+  }
+  if (p < 0) return __builtin_nan("");  // log(p < 0) in the reference
+  const double azsv = (a * w) * sv;
+  const double c = (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) * T.cden;
+  const double ec = exp(c);
+  const double r = (p * ec) * T.sc;
+  if (__builtin_isinf(ec) || (WFPT_SUBNORMAL_GUARD && r < kDblMin && r != 0))  // literal form
+    return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) /
+                             (((2.0 * (sv * sv)) * T.xx) + 2.0)) /
+            sqrt(((sv * sv) * T.xx) + 1.0)) /
+           (a * a);
+  return r;
+#endif
 }
 
 __device__ inline double pdf_sv(double xx, double v, double sv, double a, double w, double err) {
@@ -397,19 +477,23 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
     // adaptiveSimpsons_1D over z at fixed t: one t node for every evaluation
     const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
     const double ZT = ub_z - lb_z;
+    const double iZT = 1.0 / ZT;
     const TNode T = tnode_setup(x - t, v, sv, a, err);
     auto g = [&](double zc) -> double {
       ++ne;
-      return tnode_pdf_sv(T, zc, v, sv, a) / ZT;
+      return WFPT_EXACT_MATH ? tnode_pdf_sv(T, zc, v, sv, a) / ZT
+                             : tnode_pdf_sv(T, zc, v, sv, a) * iZT;
     };
     return adaptive_simpson<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, ovf, ne);
   }
   if (mode == kAdaptT) {
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
     const double ZT = ub_t - lb_t;
+    const double iZT = 1.0 / ZT;
     auto g = [&](double tc) -> double {
       ++ne;
-      return pdf_sv(x - tc, v, sv, a, z, err) / ZT;
+      return WFPT_EXACT_MATH ? pdf_sv(x - tc, v, sv, a, z, err) / ZT
+                             : pdf_sv(x - tc, v, sv, a, z, err) * iZT;
     };
     return adaptive_simpson<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, ovf, ne);
   }
@@ -418,15 +502,18 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
     const double ZT = ub_z - lb_z;
     const double stw = ub_t - lb_t;  // `st` of adaptiveSimpsons_2D (integrate.pxi:187)
+    const double iZT = 1.0 / ZT, istw = 1.0 / stw;
     const double e1 = K.simps_err;
     const int nsz = K.n_sz;
     auto outer = [&](double tc) -> double {
       const TNode T = tnode_setup(x - tc, v, sv, a, err);
       auto inner = [&](double zc) -> double {
         ++ne;
-        return tnode_pdf_sv(T, zc, v, sv, a) / ZT;
+        return WFPT_EXACT_MATH ? tnode_pdf_sv(T, zc, v, sv, a) / ZT
+                               : tnode_pdf_sv(T, zc, v, sv, a) * iZT;
       };
-      return adaptive_simpson<Stack>(inner, lb_z, ub_z, e1, nsz, ovf, ne) / stw;
+      const double r = adaptive_simpson<Stack>(inner, lb_z, ub_z, e1, nsz, ovf, ne);
+      return WFPT_EXACT_MATH ? r / stw : r * istw;
     };
     return adaptive_simpson<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, ovf, ne);
   }
@@ -438,6 +525,105 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
                              ne);
   return simpson_2d<COUNT>(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz,
                            t - st / 2., t + st / 2., K.n_st, ne);
+}
+
+// ---------------------------------------------------------------------------
+// Level-0 fast path. Most trials stop at the root interval of every adaptive
+// Simpson they run (the pinned HDDM workload: exactly 25 pdf_sv evaluations
+// per trial). fast_pdf computes exactly that part of the reference's
+// quadrature tree (prologue + root aux node, integrate.pxi:114-141 /
+// 181-206), with one evaluation site and no stacks, and reports `slow` when
+// any root test asks for refinement; such trials are recomputed by the
+// general kernel (full_pdf above). MODE: kDirect, kAdaptT, kAdaptZ, kAdaptTZ.
+
+// Root-level adaptive Simpson over z at a fixed t node: 5 evaluations.
+__device__ inline double level0_z(const TNode& T, double lb, double ub, double iZT, double serr,
+                                  int depth, double v, double sv, double a, bool& slow) {
+  const double c = (ub + lb) / 2.;
+  const double d = (lb + c) / 2., e = (c + ub) / 2.;
+  double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
+#pragma unroll 1
+  for (int i = 0; i < 5; ++i) {
+    const double p = i == 0 ? lb : i == 1 ? ub : i == 2 ? c : i == 3 ? d : e;
+    const double y = tnode_pdf_sv(T, p, v, sv, a) * iZT;
+    if (i == 0) f0 = y;
+    else if (i == 1) f1 = y;
+    else if (i == 2) f2 = y;
+    else if (i == 3) f3 = y;
+    else f4 = y;
+  }
+  const double h = ub - lb;
+  const double S = (h / 6) * ((f0 + (4 * f2)) + f1);
+  const double Sl = (h / 12) * ((f0 + (4 * f3)) + f2);
+  const double Sr = (h / 12) * ((f2 + (4 * f4)) + f1);
+  const double S2 = Sl + Sr;
+  if (!(depth <= 0 || fabs(S2 - S) <= 15 * serr)) slow = true;
+  return S2 + (S2 - S) / 15;
+}
+
+template <int MODE>
+__device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, bool& slow,
+                                  int& valid) {
+  const double a = P.a, sv = P.sv, t = P.t;
+  double v = P.v, z = P.z, st = P.st, sz = P.sz;
+  if ((z < 0) || (z > 1) || (a < 0) || (t < 0) || (st < 0) || (sv < 0) || (sz < 0) ||
+      (sz > 1) || ((fabs(x) - (t - st / 2.)) < 0) || (z + sz / 2. > 1) || (z - sz / 2. < 0) ||
+      (t - st / 2. < 0)) {
+    valid = 0;
+    return 0.0;
+  }
+  valid = 1;
+  if (x > 0) {
+    v = -v;
+    z = 1. - z;
+  }
+  x = fabs(x);
+  if (st < 1e-3) st = 0;
+  if (sz < 1e-3) sz = 0;
+  const double err = K.err;
+  if (MODE == kDirect) return pdf_sv(x - t, v, sv, a, z, err);
+  if (MODE == kAdaptZ) {
+    const double lb = z - sz / 2., ub = z + sz / 2.;
+    const TNode T = tnode_setup(x - t, v, sv, a, err);
+    return level0_z(T, lb, ub, 1.0 / (ub - lb), K.simps_err, K.n_sz, v, sv, a, slow);
+  }
+  // t outer: kAdaptT (one evaluation per t node) or kAdaptTZ (a z integral per t node)
+  const double lb = t - st / 2., ub = t + st / 2.;
+  const double c = (ub + lb) / 2.;
+  const double d = (lb + c) / 2., e = (c + ub) / 2.;
+  const double lbz = z - sz / 2., ubz = z + sz / 2.;
+  const double iZz = (MODE == kAdaptTZ) ? 1.0 / (ubz - lbz) : 0.0;
+  const double iZt = 1.0 / (ub - lb);
+  double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
+#pragma unroll 1
+  for (int j = 0; j < 5; ++j) {
+    const double tc = j == 0 ? lb : j == 1 ? ub : j == 2 ? c : j == 3 ? d : e;
+    const TNode T = tnode_setup(x - tc, v, sv, a, err);
+    double y;
+    if (MODE == kAdaptTZ) {
+      y = level0_z(T, lbz, ubz, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
+      if (slow) return 0.0;
+    } else {
+      y = tnode_pdf_sv(T, z, v, sv, a) * iZt;
+    }
+    if (j == 0) f0 = y;
+    else if (j == 1) f1 = y;
+    else if (j == 2) f2 = y;
+    else if (j == 3) f3 = y;
+    else f4 = y;
+  }
+  const double h = ub - lb;
+  const double S = (h / 6) * ((f0 + (4 * f2)) + f1);
+  const double Sl = (h / 12) * ((f0 + (4 * f3)) + f2);
+  const double Sr = (h / 12) * ((f2 + (4 * f4)) + f1);
+  const double S2 = Sl + Sr;
+  if (!(K.n_st <= 0 || fabs(S2 - S) <= 15 * K.simps_err)) slow = true;
+  return S2 + (S2 - S) / 15;
+}
+
+// evaluations of a trial that finished on the fast path (for W_trial counting)
+__host__ __device__ inline int fast_evals(int mode) {
+  return mode == kDirect ? 1 : (mode == kAdaptTZ ? 25 : 5);
 }
 
 // P(hit upper boundary), pdf.pxi:67-72

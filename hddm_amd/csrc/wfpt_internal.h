@@ -12,10 +12,14 @@ struct Knobs;
 
 int stack_kind(const Knobs& K);
 int64_t blocks_for(int64_t n);
-// out_kind: 0 = block {sum, zeros}; 1 = per-trial density (logp => log); 2 = per-trial log p
+// out_kind: 0 = block {sum, zeros}; 1 = per-trial density (logp => log); 2 = per-trial log p.
+// Adaptive modes run a level-0 fast pass then a slow pass over the deferred
+// trials: wl must hold blocks_for(n)*256 bytes and wl_n blocks_for(n) ints;
+// OUT_SUM then leaves partials_for(n) block partials in out/zeros.
 void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
                    double* out, int* zeros, unsigned long long* evals, int* status, int logp,
-                   hipStream_t s);
+                   unsigned char* wl, int* wl_n, hipStream_t s);
+int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 void launch_finalize(const double* part, const int* zeros, int64_t nb, double* out,
                      hipStream_t s);
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,

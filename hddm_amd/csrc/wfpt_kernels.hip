@@ -18,6 +18,18 @@ namespace wfpt {
 
 constexpr int kBlock = 256;
 
+// Minimum waves per SIMD requested for the level-0 fast kernel (0 = let the
+// compiler choose). 3 measured best on MI355X (tools/ab_variants.py: 0.262 vs
+// 0.286 ms per 1M full-DDM trials at 0; 4 spills too much).
+#ifndef WFPT_FAST_WAVES
+#define WFPT_FAST_WAVES 3
+#endif
+#if WFPT_FAST_WAVES > 0
+#define WFPT_FAST_BOUNDS __launch_bounds__(kBlock, WFPT_FAST_WAVES)
+#else
+#define WFPT_FAST_BOUNDS __launch_bounds__(kBlock)
+#endif
+
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
 
 __device__ inline double wave_sum(double v) {
@@ -108,6 +120,104 @@ __global__ __launch_bounds__(kBlock) void trial_kernel(TrialArgs A) {
       if (OUT == OUT_SUM) {
         A.out[blockIdx.x] = lp;
         A.zeros[blockIdx.x] = zero;
+      }
+      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
+    }
+  }
+}
+
+// Level-0 fast pass (MODE in kDirect..kAdaptTZ). Trials whose root Simpson
+// tests all pass are finished here; the others are compacted per block into
+// `wl` (lane ids, one byte each) and counted in `wl_n[block]` for slow_kernel.
+template <int MODE, bool COUNT, int OUT>
+__global__ WFPT_FAST_BOUNDS void fast_kernel(TrialArgs A, unsigned char* wl,
+                                                      int* wl_n) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  long long ne = 0;
+  double lp = 0.0;
+  int zero = 0;
+  bool slow = false;
+  if (i < A.n) {
+    int valid = 0;
+    double p = fast_pdf<MODE>(A.x[i], A.P, A.K, slow, valid);
+    if (!slow) {
+      if (COUNT && valid) ne = fast_evals(MODE);
+      if (OUT == OUT_ARRAY) {
+        p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
+        A.out[i] = A.logp ? log(p) : p;
+      } else {
+        p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
+        if (p == 0) zero = 1;
+        else lp = log(p);
+        if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+      }
+    }
+  }
+  if (MODE != kDirect) {
+    // per-block compaction of the slow lanes (wave ballot + LDS prefix)
+    __shared__ int wave_cnt[kBlock / 64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long b = __ballot(slow);
+    const int before = __popcll(b & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[w] = __popcll(b);
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < w; ++k) base += wave_cnt[k];
+    if (slow) wl[(int64_t)blockIdx.x * kBlock + base + before] = (unsigned char)threadIdx.x;
+    if (threadIdx.x == 0)
+      wl_n[blockIdx.x] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+  }
+  if (OUT == OUT_SUM || COUNT) {
+    block_reduce<COUNT>(lp, zero, ne);
+    if (threadIdx.x == 0) {
+      if (OUT == OUT_SUM) {
+        A.out[blockIdx.x] = lp;
+        A.zeros[blockIdx.x] = zero;
+      }
+      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
+    }
+  }
+}
+
+// General pass over the trials the fast pass deferred: block b runs the
+// wl_n[b] slow trials of fast block b on its first wl_n[b] lanes (full
+// adaptive quadrature, reference recursion order). OUT_SUM partials go to
+// A.out[nb + b] / A.zeros[nb + b] so the finalize sum stays in fixed order.
+template <int MODE, int STK, bool COUNT, int OUT>
+__global__ __launch_bounds__(kBlock) void slow_kernel(TrialArgs A, const unsigned char* wl,
+                                                      const int* wl_n, int64_t nb) {
+  using Stack = typename StackOf<STK>::type;
+  const int cnt = wl_n[blockIdx.x];
+  if (cnt == 0) {
+    if (OUT == OUT_SUM && threadIdx.x == 0) {
+      A.out[nb + blockIdx.x] = 0.0;
+      A.zeros[nb + blockIdx.x] = 0;
+    }
+    return;
+  }
+  long long ne = 0;
+  double lp = 0.0;
+  int zero = 0, ovf = 0;
+  if ((int)threadIdx.x < cnt) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + wl[(int64_t)blockIdx.x * kBlock + threadIdx.x];
+    double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
+    if (ovf) atomicOr(A.status, ovf);
+    if (OUT == OUT_ARRAY) {
+      p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);
+      A.out[i] = A.logp ? log(p) : p;
+    } else {
+      p = p * (1 - A.P.p_outlier) + A.wp_outlier;
+      if (p == 0) zero = 1;
+      else lp = log(p);
+      if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+    }
+  }
+  if (OUT == OUT_SUM || COUNT) {
+    block_reduce<COUNT>(lp, zero, ne);
+    if (threadIdx.x == 0) {
+      if (OUT == OUT_SUM) {
+        A.out[nb + blockIdx.x] = lp;
+        A.zeros[nb + blockIdx.x] = zero;
       }
       if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
     }
@@ -242,43 +352,55 @@ __global__ __launch_bounds__(kBlock) void multi_kernel(const double* x, int64_t 
 // ---------------------------------------------------------------------------
 // launchers
 
-template <int MODE, int STK, bool COUNT>
-static void launch_mode(int out_kind, const TrialArgs& A, int64_t nb, hipStream_t s) {
-  switch (out_kind) {
-    case OUT_SUM:
-      hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT_SUM>), dim3(nb), dim3(kBlock), 0, s,
-                         A);
-      break;
-    case OUT_ARRAY:
-      hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT_ARRAY>), dim3(nb), dim3(kBlock), 0,
-                         s, A);
-      break;
-    default:
-      hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT_LOGP>), dim3(nb), dim3(kBlock), 0,
-                         s, A);
-      break;
-  }
+template <int MODE, int STK, bool COUNT, int OUT>
+static void launch_generic(const TrialArgs& A, int64_t nb, hipStream_t s) {
+  hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A);
 }
 
-template <int MODE, bool COUNT>
-static void launch_stk(int stk, int out_kind, const TrialArgs& A, int64_t nb, hipStream_t s) {
-  if (stk == 0) launch_mode<MODE, 0, COUNT>(out_kind, A, nb, s);
-  else if (stk == 1) launch_mode<MODE, 1, COUNT>(out_kind, A, nb, s);
-  else launch_mode<MODE, 2, COUNT>(out_kind, A, nb, s);
+// fast pass + (for adaptive modes) the slow pass on the deferred trials
+template <int MODE, bool COUNT, int OUT>
+static void launch_two_pass(int stk, const TrialArgs& A, int64_t nb, unsigned char* wl,
+                            int* wl_n, hipStream_t s) {
+  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl, wl_n);
+  if (MODE == kDirect) return;
+  if (stk == 0)
+    hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+                       wl_n, nb);
+  else if (stk == 1)
+    hipLaunchKernelGGL((slow_kernel<MODE, 1, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+                       wl_n, nb);
+  else
+    hipLaunchKernelGGL((slow_kernel<MODE, 2, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+                       wl_n, nb);
+}
+
+template <bool COUNT, int OUT>
+static void launch_out(int mode, int stk, const TrialArgs& A, int64_t nb, unsigned char* wl,
+                       int* wl_n, hipStream_t s) {
+  switch (mode) {
+    case kDirect: launch_two_pass<kDirect, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
+    case kAdaptT: launch_two_pass<kAdaptT, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
+    case kAdaptZ: launch_two_pass<kAdaptZ, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
+    case kAdaptTZ: launch_two_pass<kAdaptTZ, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
+    case kFixedT: launch_generic<kFixedT, 0, COUNT, OUT>(A, nb, s); break;
+    case kFixedZ: launch_generic<kFixedZ, 0, COUNT, OUT>(A, nb, s); break;
+    default: launch_generic<kFixedTZ, 0, COUNT, OUT>(A, nb, s); break;
+  }
 }
 
 template <bool COUNT>
-static void launch_all(int mode, int stk, int out_kind, const TrialArgs& A, int64_t nb,
-                       hipStream_t s) {
-  switch (mode) {
-    case kDirect: launch_mode<kDirect, 0, COUNT>(out_kind, A, nb, s); break;
-    case kAdaptT: launch_stk<kAdaptT, COUNT>(stk, out_kind, A, nb, s); break;
-    case kAdaptZ: launch_stk<kAdaptZ, COUNT>(stk, out_kind, A, nb, s); break;
-    case kAdaptTZ: launch_stk<kAdaptTZ, COUNT>(stk, out_kind, A, nb, s); break;
-    case kFixedT: launch_mode<kFixedT, 0, COUNT>(out_kind, A, nb, s); break;
-    case kFixedZ: launch_mode<kFixedZ, 0, COUNT>(out_kind, A, nb, s); break;
-    default: launch_mode<kFixedTZ, 0, COUNT>(out_kind, A, nb, s); break;
-  }
+static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, int64_t nb,
+                         unsigned char* wl, int* wl_n, hipStream_t s) {
+  if (out_kind == OUT_SUM) launch_out<COUNT, OUT_SUM>(mode, stk, A, nb, wl, wl_n, s);
+  else if (out_kind == OUT_ARRAY) launch_out<COUNT, OUT_ARRAY>(mode, stk, A, nb, wl, wl_n, s);
+  else launch_out<COUNT, OUT_LOGP>(mode, stk, A, nb, wl, wl_n, s);
+}
+
+// number of block partials launch_trials(OUT_SUM) leaves for finalize
+int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  const int64_t nb = blocks_for(n);
+  return (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) ? 2 * nb : nb;
 }
 
 int stack_kind(const Knobs& K) {
@@ -290,7 +412,7 @@ int64_t blocks_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
 void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
                    double* out, int* zeros, unsigned long long* evals, int* status, int logp,
-                   hipStream_t s) {
+                   unsigned char* wl, int* wl_n, hipStream_t s) {
   TrialArgs A;
   A.x = x;
   A.n = n;
@@ -305,8 +427,8 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   const int64_t nb = blocks_for(n);
   if (nb == 0) return;
-  if (evals) launch_all<true>(mode, stack_kind(K), out_kind, A, nb, s);
-  else launch_all<false>(mode, stack_kind(K), out_kind, A, nb, s);
+  if (evals) launch_count<true>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s);
+  else launch_count<false>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s);
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, double* out,
