@@ -175,10 +175,12 @@ int check_status(wfpt_ctx* c) {
   return WFPT_OK;
 }
 
+// Worklists: one byte per trial slot and one count per fast block; blocks own
+// 256 trials (1-D kernels) or 64 (outer-t split), so size for the finer one.
 int reserve_worklist(wfpt_ctx* c, int64_t n) {
-  const int64_t nb = wfpt::blocks_for(n);
-  HIP_TRY(c->wl.reserve(std::max<int64_t>(nb * 256, 1)));
-  HIP_TRY(c->wl_n.reserve(std::max<int64_t>(nb, 1)));
+  const int64_t nb64 = (n + 63) / 64;
+  HIP_TRY(c->wl.reserve(std::max<int64_t>(nb64 * 64 + 256, 1)));
+  HIP_TRY(c->wl_n.reserve(std::max<int64_t>(nb64, 1)));
   return WFPT_OK;
 }
 

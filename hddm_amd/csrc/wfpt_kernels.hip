@@ -29,6 +29,15 @@ constexpr int kBlock = 256;
 #else
 #define WFPT_FAST_BOUNDS __launch_bounds__(kBlock)
 #endif
+// outer-t split kernel: 320-thread blocks (5 waves); min waves per SIMD knob
+#ifndef WFPT_FAST_T_WAVES
+#define WFPT_FAST_T_WAVES 0
+#endif
+#if WFPT_FAST_T_WAVES > 0
+#define WFPT_FAST_T_BOUNDS __launch_bounds__(320, WFPT_FAST_T_WAVES)
+#else
+#define WFPT_FAST_T_BOUNDS __launch_bounds__(320)
+#endif
 
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
 
@@ -179,13 +188,74 @@ __global__ WFPT_FAST_BOUNDS void fast_kernel(TrialArgs A, unsigned char* wl,
   }
 }
 
+// Outer-t split fast pass (kAdaptT, kAdaptTZ): a block of 5 waves owns 64
+// consecutive trials; wave j evaluates t node j of every trial (t-node-major,
+// so each wave sees one |rt|-sorted run and one series branch), the node values
+// meet in LDS and wave 0 finishes the outer Simpson step, the mixture, the log
+// and the block partial. Deferred trials go to wl/wl_n with 64 slots per block.
+constexpr int kTpb = 64;  // trials per outer-t block
+
+template <int MODE, bool COUNT, int OUT>
+__global__ WFPT_FAST_T_BOUNDS void fast_t_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
+  __shared__ double F[5][kTpb];
+  __shared__ int SL[5][kTpb];
+  const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * kTpb + lane;
+  const bool in = i < A.n;
+  const double xi = in ? A.x[i] : 0.0;
+  const TrialPrep R = prepare_trial(xi, A.P);
+  bool slow = false;
+  double f = 0.0;
+  if (in && R.valid) f = fast_t_node<MODE>(R, j, A.P, A.K, slow);
+  F[j][lane] = f;
+  SL[j][lane] = slow;
+  __syncthreads();
+  if (j != 0) return;
+  slow = (SL[0][lane] | SL[1][lane] | SL[2][lane] | SL[3][lane] | SL[4][lane]) != 0;
+  double p = 0.0;
+  if (in && R.valid && !slow)
+    p = fast_t_combine(F[0][lane], F[1][lane], F[2][lane], F[3][lane], F[4][lane], R, A.P, A.K,
+                       slow);
+  slow = slow && in && R.valid;
+  long long ne = (COUNT && in && R.valid && !slow) ? fast_evals(MODE) : 0;
+  double lp = 0.0;
+  int zero = 0;
+  if (in && !slow) {
+    if (OUT == OUT_ARRAY) {
+      p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
+      A.out[i] = A.logp ? log(p) : p;
+    } else {
+      p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
+      if (p == 0) zero = 1;
+      else lp = log(p);
+      if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+    }
+  }
+  const unsigned long long b = __ballot(slow);
+  if (slow) wl[(int64_t)blockIdx.x * kTpb + __popcll(b & ((1ull << lane) - 1ull))] =
+      (unsigned char)lane;
+  if (lane == 0) wl_n[blockIdx.x] = __popcll(b);
+  if (OUT == OUT_SUM || COUNT) {
+    lp = wave_sum(lp);
+    const int zs = __popcll(__ballot(zero != 0));
+    if (COUNT) ne = wave_sum_ll(ne);
+    if (lane == 0) {
+      if (OUT == OUT_SUM) {
+        A.out[blockIdx.x] = lp;
+        A.zeros[blockIdx.x] = zs;
+      }
+      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
+    }
+  }
+}
+
 // General pass over the trials the fast pass deferred: block b runs the
 // wl_n[b] slow trials of fast block b on its first wl_n[b] lanes (full
 // adaptive quadrature, reference recursion order). OUT_SUM partials go to
 // A.out[nb + b] / A.zeros[nb + b] so the finalize sum stays in fixed order.
-template <int MODE, int STK, bool COUNT, int OUT>
-__global__ __launch_bounds__(kBlock) void slow_kernel(TrialArgs A, const unsigned char* wl,
-                                                      const int* wl_n, int64_t nb) {
+template <int MODE, int STK, bool COUNT, int OUT, int TPB>
+__global__ __launch_bounds__(TPB) void slow_kernel(TrialArgs A, const unsigned char* wl,
+                                                   const int* wl_n, int64_t nb) {
   using Stack = typename StackOf<STK>::type;
   const int cnt = wl_n[blockIdx.x];
   if (cnt == 0) {
@@ -199,7 +269,7 @@ __global__ __launch_bounds__(kBlock) void slow_kernel(TrialArgs A, const unsigne
   double lp = 0.0;
   int zero = 0, ovf = 0;
   if ((int)threadIdx.x < cnt) {
-    const int64_t i = (int64_t)blockIdx.x * kBlock + wl[(int64_t)blockIdx.x * kBlock + threadIdx.x];
+    const int64_t i = (int64_t)blockIdx.x * TPB + wl[(int64_t)blockIdx.x * TPB + threadIdx.x];
     double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
     if (ovf) atomicOr(A.status, ovf);
     if (OUT == OUT_ARRAY) {
@@ -213,7 +283,13 @@ __global__ __launch_bounds__(kBlock) void slow_kernel(TrialArgs A, const unsigne
     }
   }
   if (OUT == OUT_SUM || COUNT) {
-    block_reduce<COUNT>(lp, zero, ne);
+    if (TPB == kBlock) {
+      block_reduce<COUNT>(lp, zero, ne);
+    } else {  // one wave
+      lp = wave_sum(lp);
+      zero = __popcll(__ballot(zero != 0));
+      if (COUNT) ne = wave_sum_ll(ne);
+    }
     if (threadIdx.x == 0) {
       if (OUT == OUT_SUM) {
         A.out[nb + blockIdx.x] = lp;
@@ -358,19 +434,36 @@ static void launch_generic(const TrialArgs& A, int64_t nb, hipStream_t s) {
 }
 
 // fast pass + (for adaptive modes) the slow pass on the deferred trials
+// Outer-t split (fast_t_kernel) is a build knob: on MI355X it measured
+// 0.35-0.47 ms vs 0.254-0.267 ms per 1M full-DDM trials for the per-trial
+// fast kernel (5-wave blocks, lower resident waves), so it is off by default.
+#ifndef WFPT_T_SPLIT
+#define WFPT_T_SPLIT 0
+#endif
+constexpr bool t_split(int mode) {
+  return WFPT_T_SPLIT && (mode == kAdaptT || mode == kAdaptTZ);
+}
+
 template <int MODE, bool COUNT, int OUT>
-static void launch_two_pass(int stk, const TrialArgs& A, int64_t nb, unsigned char* wl,
+static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned char* wl,
                             int* wl_n, hipStream_t s) {
-  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl, wl_n);
+  constexpr int TPB = t_split(MODE) ? kTpb : kBlock;
+  const int64_t nb = (n + TPB - 1) / TPB;
+  if (t_split(MODE))
+    hipLaunchKernelGGL((fast_t_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(5 * kTpb), 0, s, A, wl,
+                       wl_n);
+  else
+    hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+                       wl_n);
   if (MODE == kDirect) return;
   if (stk == 0)
-    hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+    hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
                        wl_n, nb);
   else if (stk == 1)
-    hipLaunchKernelGGL((slow_kernel<MODE, 1, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+    hipLaunchKernelGGL((slow_kernel<MODE, 1, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
                        wl_n, nb);
   else
-    hipLaunchKernelGGL((slow_kernel<MODE, 2, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
+    hipLaunchKernelGGL((slow_kernel<MODE, 2, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
                        wl_n, nb);
 }
 
@@ -378,10 +471,10 @@ template <bool COUNT, int OUT>
 static void launch_out(int mode, int stk, const TrialArgs& A, int64_t nb, unsigned char* wl,
                        int* wl_n, hipStream_t s) {
   switch (mode) {
-    case kDirect: launch_two_pass<kDirect, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
-    case kAdaptT: launch_two_pass<kAdaptT, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
-    case kAdaptZ: launch_two_pass<kAdaptZ, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
-    case kAdaptTZ: launch_two_pass<kAdaptTZ, COUNT, OUT>(stk, A, nb, wl, wl_n, s); break;
+    case kDirect: launch_two_pass<kDirect, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
+    case kAdaptT: launch_two_pass<kAdaptT, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
+    case kAdaptZ: launch_two_pass<kAdaptZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
+    case kAdaptTZ: launch_two_pass<kAdaptTZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
     case kFixedT: launch_generic<kFixedT, 0, COUNT, OUT>(A, nb, s); break;
     case kFixedZ: launch_generic<kFixedZ, 0, COUNT, OUT>(A, nb, s); break;
     default: launch_generic<kFixedTZ, 0, COUNT, OUT>(A, nb, s); break;
@@ -399,8 +492,9 @@ static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, in
 // number of block partials launch_trials(OUT_SUM) leaves for finalize
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  if (t_split(mode)) return 2 * ((n + kTpb - 1) / kTpb);
   const int64_t nb = blocks_for(n);
-  return (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) ? 2 * nb : nb;
+  return mode == kAdaptZ ? 2 * nb : nb;
 }
 
 int stack_kind(const Knobs& K) {

@@ -17,9 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "w0": ["WFPT_FAST_WAVES=0"],
-    "exact": ["WFPT_EXACT_MATH=1"],
-    "guard": ["WFPT_SUBNORMAL_GUARD=1"],
+    "t4": ["WFPT_FAST_T_WAVES=4"],
+    "t5": ["WFPT_FAST_T_WAVES=5"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 

@@ -6,6 +6,8 @@ export TMPDIR=/tmp
 OUT=gpurun_out/prof
 mkdir -p $OUT
 B="python3 bench.py --steps ${STEPS:-20} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
+timeout -k 10 300 python3 bench.py --steps 30 --warmup 3 --cpu-seconds 10 > $OUT/bench_plain.log 2>&1 || { echo "BENCH_FAIL rc=$?"; exit 1; }
+echo bench-ok
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o trace -- $B > $OUT/trace_bench.log 2>&1 || { echo "TRACE_FAIL rc=$?"; exit 1; }
 echo trace-ok
