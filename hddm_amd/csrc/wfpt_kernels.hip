@@ -494,7 +494,7 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   if (t_split(mode)) return 2 * ((n + kTpb - 1) / kTpb);
   const int64_t nb = blocks_for(n);
-  return mode == kAdaptZ ? 2 * nb : nb;
+  return (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) ? 2 * nb : nb;
 }
 
 int stack_kind(const Knobs& K) {

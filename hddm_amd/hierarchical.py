@@ -1,0 +1,389 @@
+"""Hierarchical DDM sampler that scores every observed node in one launch.
+
+The reference builds the model with kabuki + PyMC 2 (hddm/models/base.py,
+hddm_info.py) and samples node by node: each slice step of one subject
+parameter calls `wfpt_like` on that subject's nodes (likelihoods.py:52-73),
+i.e. thousands of tiny CPU likelihood calls per sweep. Neither kabuki nor
+PyMC is available here, so this module restates the model and its step
+methods around the batched GPU likelihood:
+
+* model (informative HDDM, hddm_info.py:121-140; families base.py:578-690):
+    a_subj ~ Gamma(mean=a, sd=a_std),  a ~ Gamma(mean 1.5, sd 0.75), a_std ~ HalfNormal(sd 2)
+    v_subj ~ Normal(v, v_std),         v ~ Normal(2, sd 3),          v_std ~ HalfNormal(sd 2)
+    t_subj ~ Gamma(mean=t, sd=t_std),  t ~ Gamma(mean .4, sd .2),    t_std ~ HalfNormal(sd 1)
+    sv ~ HalfNormal(sd 2), sz ~ Beta(1, 3), st ~ HalfNormal(sd .3)   (group only, if included)
+    z = 0.5, p_outlier = 0.05 (base.py:687-752)
+  `depends_on={'v': 'cond'}` splits a family per condition level (kabuki), with
+  one shared std node (std_depends=False, base.py:614).
+* step methods (hddm_info.py:163-175): the group mean of a Normal family with
+  Normal children is Gibbs-updated (kNormalNormal); everything else is
+  slice-sampled (stepping out + shrinkage, Neal 2003) with the reference's
+  slice widths (hddm_info.py:103-105).
+* batching: subject-level parameters of one kind are conditionally
+  independent given the group level, so all of them take their slice step
+  together (a block Gibbs update with the same stationary distribution as the
+  reference's one-at-a-time sweep); each evaluation of the slice is ONE call
+  of `Dataset.wiener_like_nodes` over all (subject x condition) nodes.
+
+Model-level parity with the reference sampler is unpinned (PyMC/kabuki are
+absent); the per-node log-likelihood it uses is pinned to the reference via
+tests/test_hierarchical.py.
+"""
+import time
+
+import numpy as np
+from scipy import special
+
+from . import wfpt as _wfpt
+
+SLICE_WIDTHS = {"a": 1, "t": 0.01, "a_std": 1, "t_std": 0.15, "sz": 1.1, "v": 1.5, "st": 0.1,
+                "sv": 3, "v_std": 1}  # hddm_info.py:103-105
+WIENER_PARAMS = {"err": 1e-4, "n_st": 2, "n_sz": 2, "use_adaptive": 1, "simps_err": 1e-3,
+                 "w_outlier": 0.1}  # base.py:712-716
+
+
+# ---------------------------------------------------------------- log densities
+
+def gamma_logpdf_mean_sd(x, mean, sd):
+    """pm.Gamma(alpha=mean^2/sd^2, beta=mean/sd^2) (base.py:642-667)."""
+    x = np.asarray(x, dtype=np.float64)
+    shape = mean ** 2 / sd ** 2
+    rate = mean / sd ** 2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        out = shape * np.log(rate) - special.gammaln(shape) + (shape - 1) * np.log(x) - rate * x
+    return np.where(x > 0, out, -np.inf)
+
+
+def normal_logpdf(x, mu, sd):
+    return -0.5 * np.log(2 * np.pi * sd ** 2) - 0.5 * ((x - mu) / sd) ** 2
+
+
+def halfnormal_logpdf(x, sd):
+    x = np.asarray(x, dtype=np.float64)
+    out = 0.5 * np.log(2 / (np.pi * sd ** 2)) - 0.5 * (x / sd) ** 2
+    return np.where(x >= 0, out, -np.inf)
+
+
+def beta_logpdf(x, a, b):
+    x = np.asarray(x, dtype=np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        out = (a - 1) * np.log(x) + (b - 1) * np.log1p(-x) - special.betaln(a, b)
+    return np.where((x > 0) & (x < 1), out, -np.inf)
+
+
+# ---------------------------------------------------------------- slice sampler
+
+def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200):
+    """Vectorised univariate slice sampling (stepping out + shrinkage).
+
+    x0: (n,) current values of n conditionally independent coordinates;
+    logp(x) -> (n,) log conditional of each coordinate evaluated at x (one
+    batched likelihood call). Returns the new values and the number of logp
+    calls used.
+    """
+    x0 = np.asarray(x0, dtype=np.float64)
+    n = x0.size
+    calls = 1
+    y = logp(x0) - rng.exponential(size=n)
+    L = x0 - w * rng.uniform(size=n)
+    R = L + w
+    if lower is not None:
+        L = np.maximum(L, lower)
+    for side in (0, 1):
+        active = np.ones(n, dtype=bool)
+        for _ in range(max_steps):
+            probe = np.where(active, L if side == 0 else R, x0)
+            f = logp(probe)
+            calls += 1
+            grow = active & (f > y)
+            if not grow.any():
+                break
+            if side == 0:
+                L = np.where(grow, L - w, L)
+                if lower is not None:
+                    L = np.maximum(L, lower)
+                    grow &= L > lower
+            else:
+                R = np.where(grow, R + w, R)
+            active = grow
+    x1 = x0.copy()
+    done = np.zeros(n, dtype=bool)
+    for _ in range(max_shrink):
+        cand = np.where(done, x1, L + rng.uniform(size=n) * (R - L))
+        f = logp(cand)
+        calls += 1
+        acc = ~done & (f > y)
+        x1 = np.where(acc, cand, x1)
+        done |= acc
+        if done.all():
+            break
+        lo = ~done & (cand < x0)
+        L = np.where(lo, cand, L)
+        R = np.where(~done & ~lo, cand, R)
+    return x1, calls
+
+
+# ---------------------------------------------------------------- the model
+
+class HDDM:
+    """HDDM(data, depends_on={'v': 'cond'}).sample(n) on one MI355X.
+
+    data: pandas DataFrame with columns rt (seconds), response (1 upper / 0
+    lower; optional when rt is already signed), subj_idx and the condition
+    columns named in depends_on.
+    """
+
+    FAMILIES = ("a", "v", "t")
+
+    def __init__(self, data, depends_on=None, include=(), p_outlier=0.05, wiener_params=None,
+                 seed=None, device=None):
+        import pandas as pd
+        self.data = data = pd.DataFrame(data).reset_index(drop=True)
+        self.depends = {k: ([v] if isinstance(v, str) else list(v))
+                        for k, v in (depends_on or {}).items()}
+        for k in self.depends:
+            if k not in self.FAMILIES + ("sv", "sz", "st"):
+                raise NotImplementedError(f"depends_on for '{k}' is not supported")
+        self.include = set(include) | {"a", "v", "t"}
+        unsupported = self.include - {"a", "v", "t", "sv", "sz", "st"}
+        if unsupported:
+            raise NotImplementedError(f"include {sorted(unsupported)} is not supported")
+        self.p_outlier = float(p_outlier)
+        self.wp = dict(WIENER_PARAMS if wiener_params is None else wiener_params)
+        self.rng = np.random.default_rng(seed)
+
+        rt = data["rt"].to_numpy(dtype=np.float64)
+        if "response" in data and not np.any(rt < 0):
+            rt = np.where(data["response"].to_numpy() == 0, -np.abs(rt), np.abs(rt))  # flip_errors
+        subj_levels = np.sort(data["subj_idx"].unique())
+        self.n_subj = len(subj_levels)
+        cond_cols = sorted({c for cs in self.depends.values() for c in cs})
+        keys = ["subj_idx"] + cond_cols
+        grp = data.groupby(keys, sort=True)
+        node_codes = grp.ngroup().to_numpy()
+        node_frame = grp.size().reset_index()[keys]
+        self.node_keys = [tuple(r) for r in node_frame.itertuples(index=False)]
+        self.n_nodes = len(node_frame)
+        self.node_subj = np.searchsorted(subj_levels, node_frame["subj_idx"].to_numpy())
+        # per family: condition level of each node and (subject, level) unit of each node
+        self.levels, self.node_level, self.node_unit, self.n_units = {}, {}, {}, {}
+        for fam in self.FAMILIES:
+            cols = self.depends.get(fam, [])
+            if cols:
+                g = node_frame.groupby(cols, sort=True)
+                lv_codes = g.ngroup().to_numpy()
+                self.levels[fam] = [tuple(r) for r in g.size().reset_index()[cols]
+                                    .itertuples(index=False)]
+            else:
+                lv_codes = np.zeros(self.n_nodes, dtype=np.int64)
+                self.levels[fam] = [()]
+            n_lv = len(self.levels[fam])
+            self.node_level[fam] = lv_codes
+            self.node_unit[fam] = self.node_subj * n_lv + lv_codes
+            self.n_units[fam] = self.n_subj * n_lv
+        self.dataset = _wfpt.Dataset(rt, node_id=node_codes, n_nodes=self.n_nodes, device=device)
+        self.n_trials = rt.size
+        self.likelihood_calls = 0
+        self.likelihood_seconds = 0.0
+        self._init_values()
+
+    # -- state ---------------------------------------------------------------
+    def _init_values(self):
+        """Starting values of hddm_info.py:121-140."""
+        nl = {f: len(self.levels[f]) for f in self.FAMILIES}
+        self.group = {"a": np.full(nl["a"], 1.5), "v": np.full(nl["v"], 2.0),
+                      "t": np.full(nl["t"], 0.4)}
+        self.std = {"a": 0.1, "v": 0.1, "t": 0.2}
+        self.subj = {"a": np.full(self.n_units["a"], 1.0), "v": np.full(self.n_units["v"], 2.0),
+                     "t": np.full(self.n_units["t"], 0.001)}
+        self.inter = {"sv": 1.0 if "sv" in self.include else 0.0,
+                      "sz": 0.01 if "sz" in self.include else 0.0,
+                      "st": 0.001 if "st" in self.include else 0.0}
+
+    def node_table(self, over=None):
+        """(n_nodes, 8) parameter table v, sv, a, z, sz, t, st, p_outlier."""
+        over = over or {}
+        P = np.empty((self.n_nodes, 8))
+        sub = {f: over.get(f, self.subj[f]) for f in self.FAMILIES}
+        P[:, 0] = sub["v"][self.node_unit["v"]]
+        P[:, 1] = over.get("sv", self.inter["sv"])
+        P[:, 2] = sub["a"][self.node_unit["a"]]
+        P[:, 3] = 0.5
+        P[:, 4] = over.get("sz", self.inter["sz"])
+        P[:, 5] = sub["t"][self.node_unit["t"]]
+        P[:, 6] = over.get("st", self.inter["st"])
+        P[:, 7] = self.p_outlier
+        return P
+
+    def node_logp(self, over=None):
+        t0 = time.perf_counter()
+        out = self.dataset.wiener_like_nodes(self.node_table(over), **self.wp)
+        self.likelihood_seconds += time.perf_counter() - t0
+        self.likelihood_calls += 1
+        return out
+
+    def subj_prior(self, fam, x):
+        g = self.group[fam][np.arange(self.n_units[fam]) % len(self.levels[fam])]
+        if fam == "v":
+            return normal_logpdf(x, g, self.std["v"])
+        return gamma_logpdf_mean_sd(x, g, self.std[fam])
+
+    def logp(self):
+        """Joint log density of the model at the current values."""
+        lp = float(np.sum(self.node_logp()))
+        for fam in self.FAMILIES:
+            lp += float(np.sum(self.subj_prior(fam, self.subj[fam])))
+        lp += float(np.sum(self._group_prior("a", self.group["a"])))
+        lp += float(np.sum(self._group_prior("t", self.group["t"])))
+        lp += float(np.sum(normal_logpdf(self.group["v"], 2.0, 3.0)))
+        lp += float(np.sum([halfnormal_logpdf(self.std[f], s)
+                            for f, s in (("a", 2.0), ("v", 2.0), ("t", 1.0))]))
+        return lp
+
+    @staticmethod
+    def _group_prior(fam, x):
+        return gamma_logpdf_mean_sd(x, 1.5, 0.75) if fam == "a" else gamma_logpdf_mean_sd(x, .4, .2)
+
+    # -- updates ---------------------------------------------------------------
+    def _update_subject(self, fam):
+        unit = self.node_unit[fam]
+        nu = self.n_units[fam]
+
+        def logp(x):
+            ll = np.bincount(unit, weights=self.node_logp({fam: x}), minlength=nu)
+            return ll + self.subj_prior(fam, x)
+
+        lower = 0.0 if fam in ("a", "t") else None
+        self.subj[fam], _ = slice_step(self.subj[fam], logp, SLICE_WIDTHS[fam], self.rng,
+                                       lower=lower)
+
+    def _update_group(self, fam):
+        nl = len(self.levels[fam])
+        lv = np.arange(self.n_units[fam]) % nl
+        if fam == "v":  # kNormalNormal: conjugate Normal mean (hddm_info.py:167-168)
+            tau0, mu0 = 3.0 ** -2, 2.0
+            tau = self.std["v"] ** -2
+            for k in range(nl):
+                xs = self.subj["v"][lv == k]
+                prec = tau0 + tau * xs.size
+                mean = (tau0 * mu0 + tau * xs.sum()) / prec
+                self.group["v"][k] = self.rng.normal(mean, prec ** -0.5)
+        else:
+            def logp(g):
+                out = self._group_prior(fam, g)
+                for k in range(nl):
+                    out[k] += np.sum(gamma_logpdf_mean_sd(self.subj[fam][lv == k], g[k],
+                                                          self.std[fam]))
+                return out
+            self.group[fam], _ = slice_step(self.group[fam], logp, SLICE_WIDTHS[fam], self.rng,
+                                            lower=0.0)
+        std_sd = {"a": 2.0, "v": 2.0, "t": 1.0}[fam]
+
+        def logp_std(s):
+            s = float(s[0])
+            if s <= 0:
+                return np.array([-np.inf])
+            g = self.group[fam][lv]
+            x = self.subj[fam]
+            ll = normal_logpdf(x, g, s) if fam == "v" else gamma_logpdf_mean_sd(x, g, s)
+            return np.array([float(halfnormal_logpdf(s, std_sd)) + float(np.sum(ll))])
+
+        new, _ = slice_step(np.array([self.std[fam]]), logp_std, SLICE_WIDTHS[fam + "_std"],
+                            self.rng, lower=0.0)
+        self.std[fam] = float(new[0])
+
+    def _update_inter(self, name):
+        prior = {"sv": lambda x: halfnormal_logpdf(x, 2.0), "sz": lambda x: beta_logpdf(x, 1, 3),
+                 "st": lambda x: halfnormal_logpdf(x, 0.3)}[name]
+
+        def logp(x):
+            val = float(x[0])
+            pr = float(prior(val))
+            if not np.isfinite(pr):
+                return np.array([-np.inf])
+            return np.array([pr + float(np.sum(self.node_logp({name: val})))])
+
+        new, _ = slice_step(np.array([self.inter[name]]), logp, SLICE_WIDTHS[name], self.rng,
+                            lower=0.0)
+        self.inter[name] = float(new[0])
+
+    def sweep(self):
+        """One MCMC iteration: every stochastic updated once."""
+        for fam in self.FAMILIES:
+            self._update_group(fam)
+            self._update_subject(fam)
+        for name in ("sv", "sz", "st"):
+            if name in self.include:
+                self._update_inter(name)
+
+    def sample(self, iter, burn=0, thin=1, progress=None):
+        """Run `iter` sweeps; keep every `thin`-th after `burn`. Returns traces
+        of the group-level nodes (dict name -> array)."""
+        trace = {}
+        names = []
+        for fam in self.FAMILIES:
+            for k, lv in enumerate(self.levels[fam]):
+                names.append((f"{fam}" + (f"({','.join(map(str, lv))})" if lv else ""), fam, k))
+        self.trace_subj = {f: [] for f in self.FAMILIES}
+        for name, _, _ in names:
+            trace[name] = []
+        for fam in self.FAMILIES:
+            trace[f"{fam}_std"] = []
+        for name in ("sv", "sz", "st"):
+            if name in self.include:
+                trace[name] = []
+        t0 = time.perf_counter()
+        for it in range(iter):
+            self.sweep()
+            if it >= burn and (it - burn) % thin == 0:
+                for name, fam, k in names:
+                    trace[name].append(self.group[fam][k])
+                for fam in self.FAMILIES:
+                    trace[f"{fam}_std"].append(self.std[fam])
+                    self.trace_subj[fam].append(self.subj[fam].copy())
+                for name in ("sv", "sz", "st"):
+                    if name in self.include:
+                        trace[name].append(self.inter[name])
+            if progress and (it + 1) % progress == 0:
+                el = time.perf_counter() - t0
+                print(f"  [{it + 1}/{iter}] {el:.1f}s, {self.likelihood_calls} batched "
+                      f"likelihood calls", flush=True)
+        self.trace = {k: np.asarray(v) for k, v in trace.items()}
+        self.trace_subj = {k: np.asarray(v) for k, v in self.trace_subj.items()}
+        self.sample_seconds = time.perf_counter() - t0
+        return self.trace
+
+    def gen_stats(self):
+        out = {}
+        for k, v in self.trace.items():
+            out[k] = {"mean": float(np.mean(v)), "std": float(np.std(v)),
+                      "2.5q": float(np.quantile(v, .025)), "97.5q": float(np.quantile(v, .975))}
+        return out
+
+
+def gen_data(n_subj=200, n_trials=500, conds=None, a=2.0, t=0.3, sv=0.0, sz=0.0, st=0.0,
+             jitter=0.1, seed=20261017, dt=1e-3):
+    """Synthetic hierarchical data set: per subject,
+    parameters jittered by +-`jitter` (relative), RTs drawn with the GPU
+    inverse-CDF sampler (wfpt.gen_rts_from_cdf, wfpt.pyx:323-354). Returns a
+    DataFrame with rt (signed: lower-boundary responses negative), response,
+    subj_idx, cond, plus the true subject parameters as a dict."""
+    import pandas as pd
+    conds = conds or {"c0": 0.5, "c1": 1.0}
+    rng = np.random.default_rng(seed)
+    np.random.seed(seed)
+    rows = []
+    truth = {"a": [], "t": [], "v": {c: [] for c in conds}}
+    per = n_trials // len(conds)
+    for s in range(n_subj):
+        a_s = a * (1 + jitter * rng.uniform(-1, 1))
+        t_s = t * (1 + jitter * rng.uniform(-1, 1))
+        truth["a"].append(a_s)
+        truth["t"].append(t_s)
+        for c, v in conds.items():
+            v_s = v * (1 + jitter * rng.uniform(-1, 1))
+            truth["v"][c].append(v_s)
+            x = _wfpt.gen_rts_from_cdf(v_s, sv, a_s, 0.5, sz, t_s, st, samples=per, dt=dt)
+            rows.append(pd.DataFrame({"rt": x, "response": (x > 0).astype(float),
+                                      "subj_idx": s, "cond": c}))
+    return pd.concat(rows, ignore_index=True), truth

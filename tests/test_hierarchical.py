@@ -1,0 +1,146 @@
+"""Hierarchical sampler harness (§8f row 1): slice sampler on CPU, node
+likelihoods pinned to the reference on the GPU, parameter recovery."""
+import math
+
+import numpy as np
+import pytest
+from scipy import stats
+
+
+def test_slice_step_samples_target_distribution():
+    from hddm_amd.hierarchical import slice_step, gamma_logpdf_mean_sd
+    rng = np.random.default_rng(0)
+    # 4000 independent chains of a Gamma(mean 2, sd 1) and a Normal(-1, 0.5) coordinate
+    n = 4000
+    x = np.concatenate([np.full(n, 1.0), np.full(n, 0.0)])
+
+    def logp(v):
+        return np.concatenate([gamma_logpdf_mean_sd(v[:n], 2.0, 1.0),
+                               stats.norm.logpdf(v[n:], -1.0, 0.5)])
+
+    for _ in range(25):
+        x, calls = slice_step(x, logp, 1.0, rng)
+    g, nrm = x[:n], x[n:]
+    assert abs(g.mean() - 2.0) < 0.06 and abs(g.std() - 1.0) < 0.06
+    assert abs(nrm.mean() + 1.0) < 0.03 and abs(nrm.std() - 0.5) < 0.03
+    assert stats.kstest(nrm, stats.norm(-1, 0.5).cdf).pvalue > 1e-3
+
+
+def test_slice_step_respects_lower_bound():
+    from hddm_amd.hierarchical import slice_step
+    rng = np.random.default_rng(1)
+    x = np.full(2000, 0.5)
+    lp = lambda v: np.where(v > 0, -v, -np.inf)  # Exp(1)
+    for _ in range(20):
+        x, _ = slice_step(x, lp, 1.0, rng, lower=0.0)
+    assert x.min() > 0 and abs(x.mean() - 1.0) < 0.08
+
+
+def test_prior_densities():
+    from hddm_amd import hierarchical as h
+    x = np.array([0.3, 1.0, 2.5])
+    shape, rate = 1.5 ** 2 / 0.75 ** 2, 1.5 / 0.75 ** 2
+    np.testing.assert_allclose(h.gamma_logpdf_mean_sd(x, 1.5, 0.75),
+                               stats.gamma.logpdf(x, shape, scale=1 / rate))
+    np.testing.assert_allclose(h.halfnormal_logpdf(x, 2.0), stats.halfnorm.logpdf(x, scale=2.0))
+    np.testing.assert_allclose(h.beta_logpdf(np.array([0.2]), 1, 3), stats.beta.logpdf(0.2, 1, 3))
+
+
+@pytest.mark.gpu
+def test_node_likelihoods_match_reference(gpu, oracle_lib):
+    from hddm_amd.hierarchical import HDDM, gen_data
+    data, _ = gen_data(n_subj=6, n_trials=120, seed=3)
+    m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st"), seed=0)
+    m.subj["a"][:] = np.linspace(1.6, 2.2, m.n_units["a"])
+    m.subj["v"][:] = np.linspace(-0.5, 1.5, m.n_units["v"])
+    m.subj["t"][:] = np.linspace(0.2, 0.28, m.n_units["t"])
+    m.inter.update(sv=0.3, sz=0.1, st=0.1)
+    got = m.node_logp()
+    P = m.node_table()
+    rt = data["rt"].to_numpy()
+    keys = list(zip(data["subj_idx"], data["cond"]))
+    for j, key in enumerate(m.node_keys):
+        xj = rt[[k == tuple(key) for k in keys]]
+        v, sv, a, z, sz, t, st, po = P[j]
+        terms = oracle_lib.pdf_array(xj, v, sv, a, z, sz, t, st, 1e-4, 1, 2, 2, 1, 1e-3, po, 0.1)
+        ref = math.fsum(terms)
+        assert abs(got[j] - ref) < 1e-9 * abs(ref), (j, got[j], ref)
+
+
+@pytest.mark.gpu
+def test_wfpt_like_matches_reference_semantics(gpu, oracle_lib):
+    import pandas as pd
+    from hddm_amd.likelihoods import make_wfpt_like
+    rng = np.random.default_rng(4)
+    x = rng.choice([-1.0, 1.0], 300) * (0.35 + rng.gamma(2.0, 0.4, 300))
+    like = make_wfpt_like()
+    args = (0.7, 0.2, 1.8, 0.5, 0.1, 0.3, 0.1)
+    df = pd.DataFrame({"rt": x})
+    ref = oracle_lib.wiener_like(x, *args, 1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    assert abs(like(df, *args, p_outlier=0.05) - ref) < 1e-9 * abs(ref)
+    assert abs(like(df, *args, p_outlier=0.05) - ref) < 1e-9 * abs(ref)  # resident hit
+    # missing responses: binomial on P(upper) (likelihoods.py:56-73)
+    xm = x.copy()
+    xm[:7] = 999.0
+    xm[7:10] = -999.0
+    got = like(pd.DataFrame({"rt": xm}), *args, p_outlier=0.05)
+    resp = oracle_lib.wiener_like(xm[10:], *args, 1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    v, a, z = args[0], args[2], args[3]
+    p_up = (np.exp(-2 * a * z * v) - 1) / (np.exp(-2 * a * v) - 1)
+    assert abs(got - (resp + stats.binom.logpmf(7, 10, p_up))) < 1e-8
+
+
+@pytest.mark.gpu
+def test_parameter_recovery_small_model(gpu):
+    from hddm_amd.hierarchical import HDDM, gen_data
+    data, truth = gen_data(n_subj=12, n_trials=200, seed=9)
+    m = HDDM(data, depends_on={"v": "cond"}, seed=1)
+    m.sample(150, burn=50)
+    st = m.gen_stats()
+    assert abs(st["a"]["mean"] - np.mean(truth["a"])) < 0.25
+    assert abs(st["t"]["mean"] - np.mean(truth["t"])) < 0.05
+    assert abs(st["v(c0)"]["mean"] - 0.5) < 0.35 and abs(st["v(c1)"]["mean"] - 1.0) < 0.35
+    assert st["v(c1)"]["mean"] > st["v(c0)"]["mean"]
+
+
+class _OracleDataset:
+    """Test stand-in for hddm_amd.wfpt.Dataset backed by the oracle (CPU), so
+    the model bookkeeping and sweep logic run without a GPU."""
+
+    def __init__(self, rt, node_id=None, n_nodes=None, device=None):
+        import oracle
+        self.o = oracle
+        self.rt = np.asarray(rt, dtype=np.float64)
+        self.node = np.asarray(node_id)
+        self.n_nodes = n_nodes
+
+    def wiener_like_nodes(self, P, err, n_st, n_sz, use_adaptive, simps_err, w_outlier):
+        out = np.empty(self.n_nodes)
+        for j in range(self.n_nodes):
+            v, sv, a, z, sz, t, st, po = P[j]
+            out[j] = self.o.wiener_like(self.rt[self.node == j], v, sv, a, z, sz, t, st, err,
+                                        n_st, n_sz, use_adaptive, simps_err, po, w_outlier)
+        return out
+
+
+def test_model_bookkeeping_and_sweep_on_cpu(oracle_lib, monkeypatch):
+    import pandas as pd
+    from hddm_amd import hierarchical as h
+    monkeypatch.setattr(h._wfpt, "Dataset", _OracleDataset)
+    rng = np.random.default_rng(2)
+    rows = []
+    for s in range(4):
+        for c, v in (("lo", 0.5), ("hi", 1.2)):
+            x = rng.choice([-1.0, 1.0], 60, p=[0.3, 0.7]) * (0.3 + rng.gamma(2.0, 0.3, 60))
+            rows.append(pd.DataFrame({"rt": x, "subj_idx": s, "cond": c}))
+    data = pd.concat(rows, ignore_index=True)
+    m = h.HDDM(data, depends_on={"v": "cond"}, seed=0)
+    assert m.n_nodes == 8 and m.n_units["v"] == 8 and m.n_units["a"] == 4
+    assert m.levels["v"] == [("hi",), ("lo",)]
+    P = m.node_table()
+    assert P.shape == (8, 8) and np.all(P[:, 3] == 0.5) and np.all(P[:, 7] == 0.05)
+    lp0 = m.logp()
+    assert np.isfinite(lp0)
+    m.sample(6, burn=2)
+    assert m.trace["v(hi)"].shape == (4,) and np.isfinite(m.logp())
+    assert m.likelihood_calls > 6

@@ -1,0 +1,91 @@
+"""Config-4 benchmark: hierarchical HDDM, 200 subjects x 500 trials,
+depends_on={'v': 'cond'}, sampled on one MI355X (hddm_amd.hierarchical).
+
+Prints one JSON line: sweeps/s (one sweep = every stochastic node updated
+once, as one PyMC MCMC iteration), batched likelihood calls per sweep,
+node-likelihood evaluations per second, and — for context — the reference's
+CPU cost of the same node evaluations (oracle/_ref wiener_like on one
+250-trial node x the node evaluations the sweep performed; the reference's
+PyMC/kabuki sampler itself cannot run offline, so this is an estimate of its
+likelihood time only, labelled as such).
+
+    python tools/bench_hier.py [--subjects 200] [--trials 500] [--iters 200] [--full]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--subjects", type=int, default=200)
+    ap.add_argument("--trials", type=int, default=500)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--burn", type=int, default=20)
+    ap.add_argument("--full", action="store_true", help="include sv, sz, st (full DDM)")
+    a = ap.parse_args()
+    from hddm_amd.hierarchical import HDDM, gen_data
+    t0 = time.perf_counter()
+    sv = sz = st = 0.0
+    if a.full:
+        sv, sz, st = 0.1, 0.1, 0.1
+    data, truth = gen_data(n_subj=a.subjects, n_trials=a.trials, sv=sv, sz=sz, st=st)
+    t_gen = time.perf_counter() - t0
+    m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st") if a.full else (),
+             seed=1)
+    m.sample(a.burn)  # warm-up (untimed)
+    c0, s0 = m.likelihood_calls, m.likelihood_seconds
+    t0 = time.perf_counter()
+    m.sample(a.iters)
+    el = time.perf_counter() - t0
+    calls = m.likelihood_calls - c0
+    lik_s = m.likelihood_seconds - s0
+    stats = m.gen_stats()
+    node_evals = calls * m.n_nodes
+    out = {
+        "metric": "hierarchical HDDM sweeps/sec (200 subj x 500 trials, depends_on v:cond)",
+        "value": a.iters / el, "unit": "sweeps/s",
+        "config": {"subjects": a.subjects, "trials_per_subject": a.trials,
+                   "nodes": m.n_nodes, "trials": m.n_trials, "full_ddm": a.full,
+                   "iters": a.iters},
+        "seconds": el, "extrapolated_sample_2000_s": 2000 * el / a.iters,
+        "batched_likelihood_calls_per_sweep": calls / a.iters,
+        "likelihood_fraction_of_time": lik_s / el,
+        "node_evals_per_s": node_evals / el,
+        "trial_evals_per_s": calls * m.n_trials / el,
+        "data_generation_s": t_gen,
+        "posterior": {k: stats[k]["mean"] for k in stats},
+        "truth": {"a": float(np.mean(truth["a"])), "t": float(np.mean(truth["t"])),
+                  "v(c0)": float(np.mean(truth["v"]["c0"])),
+                  "v(c1)": float(np.mean(truth["v"]["c1"]))},
+    }
+    try:
+        import oracle
+        R = oracle.load_ref()
+        if R is not None:
+            node = data["rt"].to_numpy()[: a.trials // 2]
+            p = (1.0, sv, 2.0, 0.5, sz, 0.3, st)
+            reps, t1 = 0, time.perf_counter()
+            while time.perf_counter() - t1 < 2.0:
+                R.wiener_like(node, *p, 1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+                reps += 1
+            per_node = (time.perf_counter() - t1) / reps
+            out["cpu_reference_estimate"] = {
+                "per_node_call_s": per_node, "node_size": int(node.size),
+                "likelihood_s_per_sweep": per_node * node_evals / a.iters,
+                "note": "reference Cython wiener_like per node x node evaluations of one sweep; "
+                        "excludes PyMC/kabuki overhead (not runnable offline)"}
+    except Exception as e:  # noqa: BLE001
+        out["cpu_reference_estimate"] = {"error": str(e)}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
