@@ -79,6 +79,46 @@ __host__ __device__ inline int select_mode(double sz, double st, int use_adaptiv
 constexpr double kDblMin = 2.2250738585072014e-308;
 constexpr double kSubnormalLo = -745.2, kSubnormalHi = -708.3;  // exp() subnormal band
 
+// sin(pi w) and cos(pi w) for w in [0, 1] (the only range full_pdf produces:
+// validity + flip keep every z node in [0, 1]). Exact reduction t = 2w,
+// n = rint(t), f = t - n in [-1/2, 1/2], x = f pi/2 in [-pi/4, pi/4]; Taylor
+// polynomials to x^17 / x^18 (truncation < 1e-19) by FMA Horner: <= 1.1 ulp
+// relative (checked against 120-bit arithmetic). 30 fp64 ops instead of OCML's
+// general-range sincospi (127). w == 1 is seeded with the reference's own
+// sin(fl(pi)) = 1.2246e-16 so the z = 1 edge keeps its nonzero value.
+__device__ inline void sincospi01(double w, double& s, double& c) {
+  const double t = 2.0 * w;
+  const double n = rint(t);
+  const double f = t - n;
+  const double x = f * 1.5707963267948966;  // pi/2
+  const double x2 = x * x;
+  double ps = 0x1.952c77030ad4ap-49;
+  ps = fma(ps, x2, -0x1.ae7f3e733b81fp-41);
+  ps = fma(ps, x2, 0x1.6124613a86d09p-33);
+  ps = fma(ps, x2, -0x1.ae64567f544e4p-26);
+  ps = fma(ps, x2, 0x1.71de3a556c734p-19);
+  ps = fma(ps, x2, -0x1.a01a01a01a01ap-13);
+  ps = fma(ps, x2, 0x1.1111111111111p-7);
+  ps = fma(ps, x2, -0x1.5555555555555p-3);
+  const double sx = fma(x * x2, ps, x);
+  double pc = -0x1.6827863b97d97p-53;
+  pc = fma(pc, x2, 0x1.ae7f3e733b81fp-45);
+  pc = fma(pc, x2, -0x1.93974a8c07c9dp-37);
+  pc = fma(pc, x2, 0x1.1eed8eff8d898p-29);
+  pc = fma(pc, x2, -0x1.27e4fb7789f5cp-22);
+  pc = fma(pc, x2, 0x1.a01a01a01a01ap-16);
+  pc = fma(pc, x2, -0x1.6c16c16c16c17p-10);
+  pc = fma(pc, x2, 0x1.5555555555555p-5);
+  const double cx = fma(x2 * x2, pc, fma(-0.5, x2, 1.0));
+  const bool q1 = n == 1.0, q2 = n == 2.0;
+  s = q1 ? cx : (q2 ? -sx : sx);
+  c = q1 ? -sx : (q2 ? -cx : cx);
+  if (w == 1.0) {
+    s = 1.2246467991473532e-16;  // sin(M_PI) in double, as the reference computes
+    c = -1.0;
+  }
+}
+
 struct TNode {
   double xx;    // x - t_node: the `x` argument of pdf_sv
   double tt;    // xx / a^2 (pdf.pxi:98)
@@ -110,23 +150,53 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   const double a2 = a * a;
   const double tt = xx / a2;
   T.tt = tt;
-  double kl, ks;
-  // pdf.pxi:36-40
-  if ((kPi * tt) * err < 1.0) {
-    kl = sqrt((-2.0 * log((kPi * tt) * err)) / (kPi2 * tt));
-    const double b = 1. / (kPi * sqrt(tt));
-    kl = (kl < b) ? b : kl;
-  } else {
-    kl = 1. / (kPi * sqrt(tt));
-  }
-  // pdf.pxi:43-47
+  // Series branch and term count (pdf.pxi:36-60). kl and ks feed ONLY these
+  // two decisions, so they are first computed with fp32 logs (~1e-7 abs.);
+  // when any decision is within 1e-5 of flipping — or an fp32 argument is out
+  // of range — they are recomputed with the reference's fp64 operations.
+  const double sqt = sqrt(tt);
+  const double inv_pi_sqt = 1. / (kPi * sqt);
+  const double arg_l = (kPi * tt) * err;
   const double s2pt = sqrt((2.0 * kPi) * tt);
-  if ((2.0 * s2pt) * err < 1.0) {
-    ks = 2.0 + sqrt((-2.0 * tt) * log((2.0 * s2pt) * err));
-    const double b = sqrt(tt) + 1.0;
-    ks = (ks < b) ? b : ks;
-  } else {
-    ks = 2.0;
+  const double arg_s = (2.0 * s2pt) * err;
+  const bool use_l = arg_l < 1.0, use_s = arg_s < 1.0;
+  double kl, ks;
+  bool exact = WFPT_EXACT_MATH || (use_l && !(arg_l > 1e-30)) || (use_s && !(arg_s > 1e-30));
+  if (!exact) {
+    // |dL| <~ 2e-7 (fp32 rounding of the argument + logf); the relative error
+    // it induces in kl/ks is <= |dL| / (2|L|), so |L| >= 0.1 keeps it <= 1e-6.
+    const double Ll = use_l ? (double)logf((float)arg_l) : -1.0;
+    const double Ls = use_s ? (double)logf((float)arg_s) : -1.0;
+    exact = Ll > -0.1 || Ls > -0.1;
+    kl = use_l ? sqrt((-2.0 * Ll) / (kPi2 * tt)) : inv_pi_sqt;
+    ks = use_s ? 2.0 + sqrt((-2.0 * tt) * Ls) : 2.0;
+    const double b2 = sqt + 1.0;
+    const double tol = 1e-5;
+    const bool amb_l = use_l && fabs(kl - inv_pi_sqt) <= tol * kl;
+    const bool amb_s = use_s && fabs(ks - b2) <= tol * ks;
+    if (use_l) kl = (kl < inv_pi_sqt) ? inv_pi_sqt : kl;
+    if (use_s) ks = (ks < b2) ? b2 : ks;
+    const double kk = (ks < kl) ? ks : kl;
+    const bool amb_b = fabs(ks - kl) <= tol * kl;
+    const bool amb_k = fabs(kk - rint(kk)) <= tol * kk;
+    exact = exact || amb_l || amb_s || amb_b || amb_k;
+  }
+  if (exact) {
+    // pdf.pxi:36-40
+    if (use_l) {
+      kl = sqrt((-2.0 * log(arg_l)) / (kPi2 * tt));
+      kl = (kl < inv_pi_sqt) ? inv_pi_sqt : kl;
+    } else {
+      kl = inv_pi_sqt;
+    }
+    // pdf.pxi:43-47
+    if (use_s) {
+      ks = 2.0 + sqrt((-2.0 * tt) * log(arg_s));
+      const double b = sqt + 1.0;
+      ks = (ks < b) ? b : ks;
+    } else {
+      ks = 2.0;
+    }
   }
   if (ks < kl) {
     T.small = 1;
@@ -179,7 +249,7 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
     }
 #else
     double s1, c1;
-    sincospi(w, &s1, &c1);
+    sincospi01(w, s1, c1);
     const double tc = c1 + c1;
     double sk = s1, skm1 = 0.0;          // sin(k pi w), sin((k-1) pi w)
     double e = T.m, r = T.m * T.q2;      // q^(k^2), q^(2k+1)

@@ -17,8 +17,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "t4": ["WFPT_FAST_T_WAVES=4"],
-    "t5": ["WFPT_FAST_T_WAVES=5"],
+    "exact": ["WFPT_EXACT_MATH=1"],
+    "w0": ["WFPT_FAST_WAVES=0"],
+    "w4": ["WFPT_FAST_WAVES=4"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
