@@ -300,6 +300,84 @@ __device__ inline double tnode_pdf_sv(const TNode& T, double w, double v, double
 #endif
 }
 
+// pdf_sv at N z nodes of ONE t node. The nodes share the series branch and
+// K (they depend on tt only), so the N evaluations run as N independent,
+// interleavable instruction chains under one control flow, sharing the
+// q^(k^2) recurrence and every constant. Same arithmetic as tnode_pdf_sv.
+template <int N>
+__device__ inline void tnode_pdf_sv_n(const TNode& T, const double (&w)[N], double v, double sv,
+                                      double a, double (&out)[N]) {
+  double p[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) p[i] = 0.0;
+  if (!T.pos) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = 0.0;
+    return;
+  }
+  const int K = T.K;
+  if (T.small) {
+    const int lower = (int)(-floor((K - 1) / 2.));
+    const int upper = (int)ceil((K - 1) / 2.);
+    for (int k = lower; k <= upper; ++k) {
+      const double k2 = (double)(2 * k);
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const double wk = w[i] + k2;
+        p[i] = p[i] + wk * exp((wk * wk) * T.m);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = p[i] * T.rn;
+  } else {
+    double tc[N], sk[N], skm1[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      double s1, c1;
+      sincospi01(w[i], s1, c1);
+      tc[i] = c1 + c1;
+      sk[i] = s1;
+      skm1[i] = 0.0;
+      if (K >= 1) p[i] = T.m * s1;
+    }
+    double e = T.m, r = T.m * T.q2;
+    for (int k = 2; k <= K; ++k) {
+      e = e * r;
+      r = r * T.q2;
+      const double ke = (double)k * e;
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const double sn = tc[i] * sk[i] - skm1[i];
+        skm1[i] = sk[i];
+        sk[i] = sn;
+        p[i] = p[i] + ke * sk[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = p[i] * kPi;
+  }
+  if (sv == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+      out[i] = (p[i] * exp((((-v) * a) * w[i]) - (T.vvx * 0.5))) * T.sc;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const double azsv = (a * w[i]) * sv;
+    const double c = (((azsv * azsv) - (((2.0 * a) * v) * w[i])) - T.vvx) * T.cden;
+    const double ec = exp(c);
+    double r2 = (p[i] * ec) * T.sc;
+    if (p[i] < 0) r2 = __builtin_nan("");  // log(p < 0) in the reference
+    out[i] = r2;
+  }
+  // exp(c) overflow: the reference's literal exp(log p + c) (rare, per lane)
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, w[i], v, sv, a);
+  }
+}
+
 __device__ inline double pdf_sv(double xx, double v, double sv, double a, double w, double err) {
   const TNode T = tnode_setup(xx, v, sv, a, err);
   return tnode_pdf_sv(T, w, v, sv, a);
@@ -606,26 +684,20 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
 // any root test asks for refinement; such trials are recomputed by the
 // general kernel (full_pdf above). MODE: kDirect, kAdaptT, kAdaptZ, kAdaptTZ.
 
-// Root-level adaptive Simpson over z at a fixed t node: 5 evaluations.
+// Root-level adaptive Simpson over z at a fixed t node: 5 evaluations, run
+// 5-wide (tnode_pdf_sv_n) since they share the t node's branch and K.
 __device__ inline double level0_z(const TNode& T, double lb, double ub, double iZT, double serr,
                                   int depth, double v, double sv, double a, bool& slow) {
   const double c = (ub + lb) / 2.;
-  const double d = (lb + c) / 2., e = (c + ub) / 2.;
-  double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
-#pragma unroll 1
-  for (int i = 0; i < 5; ++i) {
-    const double p = i == 0 ? lb : i == 1 ? ub : i == 2 ? c : i == 3 ? d : e;
-    const double y = tnode_pdf_sv(T, p, v, sv, a) * iZT;
-    if (i == 0) f0 = y;
-    else if (i == 1) f1 = y;
-    else if (i == 2) f2 = y;
-    else if (i == 3) f3 = y;
-    else f4 = y;
-  }
+  const double w[5] = {lb, ub, c, (lb + c) / 2., (c + ub) / 2.};
+  double f[5];
+  tnode_pdf_sv_n<5>(T, w, v, sv, a, f);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) f[i] = f[i] * iZT;
   const double h = ub - lb;
-  const double S = (h / 6) * ((f0 + (4 * f2)) + f1);
-  const double Sl = (h / 12) * ((f0 + (4 * f3)) + f2);
-  const double Sr = (h / 12) * ((f2 + (4 * f4)) + f1);
+  const double S = (h / 6) * ((f[0] + (4 * f[2])) + f[1]);
+  const double Sl = (h / 12) * ((f[0] + (4 * f[3])) + f[2]);
+  const double Sr = (h / 12) * ((f[2] + (4 * f[4])) + f[1]);
   const double S2 = Sl + Sr;
   if (!(depth <= 0 || fabs(S2 - S) <= 15 * serr)) slow = true;
   return S2 + (S2 - S) / 15;

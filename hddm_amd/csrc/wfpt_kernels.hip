@@ -18,17 +18,20 @@ namespace wfpt {
 
 constexpr int kBlock = 256;
 
-// Minimum waves per SIMD requested for the level-0 fast kernel (0 = let the
-// compiler choose). 3 measured best on MI355X (tools/ab_variants.py: 0.262 vs
-// 0.286 ms per 1M full-DDM trials at 0; 4 spills too much).
+// Minimum waves per SIMD requested for the level-0 fast kernels (0 = let the
+// compiler choose): WFPT_FAST_WAVES for the 1-D / direct modes,
+// WFPT_FAST_WAVES_TZ for the 2-D mode (5-wide z evaluation: 199 VGPRs, 2 waves
+// spill-free; 3 waves spill 36). Chosen by tools/ab_variants.py on MI355X.
 #ifndef WFPT_FAST_WAVES
 #define WFPT_FAST_WAVES 3
 #endif
-#if WFPT_FAST_WAVES > 0
-#define WFPT_FAST_BOUNDS __launch_bounds__(kBlock, WFPT_FAST_WAVES)
-#else
-#define WFPT_FAST_BOUNDS __launch_bounds__(kBlock)
+#ifndef WFPT_FAST_WAVES_TZ
+#define WFPT_FAST_WAVES_TZ 2
 #endif
+template <int MODE>
+struct FastWaves {
+  static constexpr int value = MODE == kAdaptTZ ? WFPT_FAST_WAVES_TZ : WFPT_FAST_WAVES;
+};
 // outer-t split kernel: 320-thread blocks (5 waves); min waves per SIMD knob
 #ifndef WFPT_FAST_T_WAVES
 #define WFPT_FAST_T_WAVES 0
@@ -139,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void trial_kernel(TrialArgs A) {
 // tests all pass are finished here; the others are compacted per block into
 // `wl` (lane ids, one byte each) and counted in `wl_n[block]` for slow_kernel.
 template <int MODE, bool COUNT, int OUT>
-__global__ WFPT_FAST_BOUNDS void fast_kernel(TrialArgs A, unsigned char* wl,
+__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1) void fast_kernel(TrialArgs A, unsigned char* wl,
                                                       int* wl_n) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   long long ne = 0;

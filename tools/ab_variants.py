@@ -17,9 +17,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "exact": ["WFPT_EXACT_MATH=1"],
-    "w0": ["WFPT_FAST_WAVES=0"],
-    "w4": ["WFPT_FAST_WAVES=4"],
+    "tz3": ["WFPT_FAST_WAVES_TZ=3"],
+    "tz1": ["WFPT_FAST_WAVES_TZ=1"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
