@@ -154,43 +154,53 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   // two decisions, so they are first computed with fp32 logs (~1e-7 abs.);
   // when any decision is within 1e-5 of flipping — or an fp32 argument is out
   // of range — they are recomputed with the reference's fp64 operations.
-  const double sqt = sqrt(tt);
-  const double inv_pi_sqt = 1. / (kPi * sqt);
-  const double arg_l = (kPi * tt) * err;
-  const double s2pt = sqrt((2.0 * kPi) * tt);
-  const double arg_s = (2.0 * s2pt) * err;
-  const bool use_l = arg_l < 1.0, use_s = arg_s < 1.0;
-  double kl, ks;
-  bool exact = WFPT_EXACT_MATH || (use_l && !(arg_l > 1e-30)) || (use_s && !(arg_s > 1e-30));
+  // fp32 estimate of every decision input; the fp64 reference operations run
+  // only for lanes where a decision is within 1e-5 (relative) of flipping or an
+  // input is outside the fp32 range.
+  double kl = 0.0, ks = 0.0;
+  bool use_l = false, use_s = false;
+  bool exact = WFPT_EXACT_MATH || !(tt > 1e-30 && tt < 1e30 && err > 1e-30 && err < 1e30);
   if (!exact) {
-    // |dL| <~ 2e-7 (fp32 rounding of the argument + logf); the relative error
-    // it induces in kl/ks is <= |dL| / (2|L|), so |L| >= 0.1 keeps it <= 1e-6.
-    const double Ll = use_l ? (double)logf((float)arg_l) : -1.0;
-    const double Ls = use_s ? (double)logf((float)arg_s) : -1.0;
-    exact = Ll > -0.1 || Ls > -0.1;
-    kl = use_l ? sqrt((-2.0 * Ll) / (kPi2 * tt)) : inv_pi_sqt;
-    ks = use_s ? 2.0 + sqrt((-2.0 * tt) * Ls) : 2.0;
-    const double b2 = sqt + 1.0;
-    const double tol = 1e-5;
-    const bool amb_l = use_l && fabs(kl - inv_pi_sqt) <= tol * kl;
-    const bool amb_s = use_s && fabs(ks - b2) <= tol * ks;
-    if (use_l) kl = (kl < inv_pi_sqt) ? inv_pi_sqt : kl;
-    if (use_s) ks = (ks < b2) ? b2 : ks;
-    const double kk = (ks < kl) ? ks : kl;
-    const bool amb_b = fabs(ks - kl) <= tol * kl;
-    const bool amb_k = fabs(kk - rint(kk)) <= tol * kk;
-    exact = exact || amb_l || amb_s || amb_b || amb_k;
+    const float ttf = (float)tt, errf = (float)err;
+    const float sqtf = sqrtf(ttf);
+    const float ipsf = 1.0f / ((float)kPi * sqtf);
+    const float argl = ((float)kPi * ttf) * errf;
+    const float args = (2.0f * sqrtf((2.0f * (float)kPi) * ttf)) * errf;
+    use_l = argl < 1.0f;
+    use_s = args < 1.0f;
+    const float tol = 1e-5f;
+    // |dL| <~ 2e-7 from fp32 rounding + logf; the relative error it induces in
+    // kl/ks is <= |dL| / (2|L|), so |L| >= 0.1 keeps it <= 1e-6 (10x inside tol).
+    const float Ll = use_l ? logf(argl) : -1.0f;
+    const float Ls = use_s ? logf(args) : -1.0f;
+    float klf = use_l ? sqrtf((-2.0f * Ll) / ((float)kPi2 * ttf)) : ipsf;
+    float ksf = use_s ? 2.0f + sqrtf((-2.0f * ttf) * Ls) : 2.0f;
+    const float b2 = sqtf + 1.0f;
+    const bool amb_t = fabsf(argl - 1.0f) <= tol || fabsf(args - 1.0f) <= tol;
+    const bool amb_l = use_l && fabsf(klf - ipsf) <= tol * klf;
+    const bool amb_s = use_s && fabsf(ksf - b2) <= tol * ksf;
+    if (use_l) klf = (klf < ipsf) ? ipsf : klf;
+    if (use_s) ksf = (ksf < b2) ? b2 : ksf;
+    const float kk = (ksf < klf) ? ksf : klf;
+    const bool amb_b = fabsf(ksf - klf) <= tol * klf;
+    const bool amb_k = fabsf(kk - rintf(kk)) <= tol * kk;
+    const bool rng = (use_l && !(argl > 1e-30f)) || (use_s && !(args > 1e-30f));
+    exact = rng || Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k;
+    kl = klf;
+    ks = ksf;
   }
-  if (exact) {
-    // pdf.pxi:36-40
-    if (use_l) {
+  if (exact) {  // the reference's fp64 operations, pdf.pxi:36-47
+    const double sqt = sqrt(tt);
+    const double inv_pi_sqt = 1. / (kPi * sqt);
+    const double arg_l = (kPi * tt) * err;
+    const double arg_s = (2.0 * sqrt((2.0 * kPi) * tt)) * err;
+    if (arg_l < 1.0) {
       kl = sqrt((-2.0 * log(arg_l)) / (kPi2 * tt));
       kl = (kl < inv_pi_sqt) ? inv_pi_sqt : kl;
     } else {
       kl = inv_pi_sqt;
     }
-    // pdf.pxi:43-47
-    if (use_s) {
+    if (arg_s < 1.0) {
       ks = 2.0 + sqrt((-2.0 * tt) * log(arg_s));
       const double b = sqt + 1.0;
       ks = (ks < b) ? b : ks;

@@ -139,12 +139,17 @@ __global__ __launch_bounds__(kBlock) void trial_kernel(TrialArgs A) {
 }
 
 // Level-0 fast pass (MODE in kDirect..kAdaptTZ). Trials whose root Simpson
-// tests all pass are finished here; the others are compacted per block into
-// `wl` (lane ids, one byte each) and counted in `wl_n[block]` for slow_kernel.
+// tests all pass are finished here; the others are compacted per WAVE into
+// `wl` (lane ids, one byte each, 64 slots per wave) and counted in
+// `wl_n[wave]` for slow_kernel. Barrier-free: every wave writes its own
+// partial sum / zero count (A.out[wave], A.zeros[wave]) and worklist, so a
+// wave that finishes early never waits for its block.
 template <int MODE, bool COUNT, int OUT>
-__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1) void fast_kernel(TrialArgs A, unsigned char* wl,
-                                                      int* wl_n) {
+__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t wave = i >> 6;
+  const int lane = threadIdx.x & 63;
   long long ne = 0;
   double lp = 0.0;
   int zero = 0;
@@ -166,25 +171,18 @@ __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE
     }
   }
   if (MODE != kDirect) {
-    // per-block compaction of the slow lanes (wave ballot + LDS prefix)
-    __shared__ int wave_cnt[kBlock / 64];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const unsigned long long b = __ballot(slow);
-    const int before = __popcll(b & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_cnt[w] = __popcll(b);
-    __syncthreads();
-    int base = 0;
-    for (int k = 0; k < w; ++k) base += wave_cnt[k];
-    if (slow) wl[(int64_t)blockIdx.x * kBlock + base + before] = (unsigned char)threadIdx.x;
-    if (threadIdx.x == 0)
-      wl_n[blockIdx.x] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
+    if (slow) wl[wave * 64 + __popcll(b & ((1ull << lane) - 1ull))] = (unsigned char)lane;
+    if (lane == 0) wl_n[wave] = __popcll(b);
   }
   if (OUT == OUT_SUM || COUNT) {
-    block_reduce<COUNT>(lp, zero, ne);
-    if (threadIdx.x == 0) {
+    lp = wave_sum(lp);
+    const int zs = __popcll(__ballot(zero != 0));
+    if (COUNT) ne = wave_sum_ll(ne);
+    if (lane == 0) {
       if (OUT == OUT_SUM) {
-        A.out[blockIdx.x] = lp;
-        A.zeros[blockIdx.x] = zero;
+        A.out[wave] = lp;
+        A.zeros[wave] = zs;
       }
       if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
     }
@@ -450,14 +448,15 @@ constexpr bool t_split(int mode) {
 template <int MODE, bool COUNT, int OUT>
 static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned char* wl,
                             int* wl_n, hipStream_t s) {
-  constexpr int TPB = t_split(MODE) ? kTpb : kBlock;
+  // both fast kernels leave one partial / worklist per 64 trials
+  constexpr int TPB = 64;
   const int64_t nb = (n + TPB - 1) / TPB;
   if (t_split(MODE))
     hipLaunchKernelGGL((fast_t_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(5 * kTpb), 0, s, A, wl,
                        wl_n);
   else
-    hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A, wl,
-                       wl_n);
+    hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
+                       A, wl, wl_n);
   if (MODE == kDirect) return;
   if (stk == 0)
     hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
@@ -495,9 +494,10 @@ static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, in
 // number of block partials launch_trials(OUT_SUM) leaves for finalize
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  if (t_split(mode)) return 2 * ((n + kTpb - 1) / kTpb);
-  const int64_t nb = blocks_for(n);
-  return (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) ? 2 * nb : nb;
+  const int64_t nw = (n + 63) / 64;  // fast (and slow) partials are per 64 trials
+  if (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) return 2 * nw;
+  if (mode == kDirect) return nw;
+  return blocks_for(n);  // fixed Simpson: trial_kernel, one partial per 256-trial block
 }
 
 int stack_kind(const Knobs& K) {

@@ -17,8 +17,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "tz3": ["WFPT_FAST_WAVES_TZ=3"],
-    "tz1": ["WFPT_FAST_WAVES_TZ=1"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
