@@ -694,20 +694,135 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
 // any root test asks for refinement; such trials are recomputed by the
 // general kernel (full_pdf above). MODE: kDirect, kAdaptT, kAdaptZ, kAdaptTZ.
 
+// pdf_sv at the 5 root-level z nodes of one t node, ordered as the equally
+// spaced grid g_j = lb + j (ub - lb) / 4, j = 0..4 (lb, d, c, e, ub). Same
+// values as tnode_pdf_sv_n<5> to a few ulp, using the grid structure:
+//   * large-t: sin/cos(pi g_j) for j = 1..3 by angle-addition rotation from
+//     the directly evaluated g_0; g_4 = ub is evaluated directly so the
+//     w = 1 edge keeps the reference's own sin(pi) value;
+//   * the sv factor exp(c(g_j)), c quadratic in g: 3 exponentials and the
+//     second-difference recurrence (direct exps when |c| > 600).
+// g[] holds the reference's own node coordinates (used for every polynomial
+// in w); only the transcendental factors use the recurrences.
+__device__ inline void tnode_pdf_sv_grid5(const TNode& T, const double (&g)[5], double v,
+                                          double sv, double a, double (&out)[5]) {
+  double p[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) p[i] = 0.0;
+  if (!T.pos) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) out[i] = 0.0;
+    return;
+  }
+  const int K = T.K;
+  if (T.small) {
+    const int lower = (int)(-floor((K - 1) / 2.));
+    const int upper = (int)ceil((K - 1) / 2.);
+    for (int k = lower; k <= upper; ++k) {
+      const double k2 = (double)(2 * k);
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const double wk = g[i] + k2;
+        p[i] = p[i] + wk * exp((wk * wk) * T.m);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) p[i] = p[i] * T.rn;
+  } else {
+    double sj[5], cj[5];
+    sincospi01(g[0], sj[0], cj[0]);
+    sincospi01(g[4], sj[4], cj[4]);
+    double sd, cd;
+    sincospi01((g[4] - g[0]) * 0.25, sd, cd);
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      sj[j] = fma(sj[j - 1], cd, cj[j - 1] * sd);
+      cj[j] = fma(cj[j - 1], cd, -(sj[j - 1] * sd));
+    }
+    double tc[5], sk[5], skm1[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      tc[i] = cj[i] + cj[i];
+      sk[i] = sj[i];
+      skm1[i] = 0.0;
+      if (K >= 1) p[i] = T.m * sj[i];
+    }
+    double e = T.m, r = T.m * T.q2;
+    for (int k = 2; k <= K; ++k) {
+      e = e * r;
+      r = r * T.q2;
+      const double ke = (double)k * e;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const double sn = tc[i] * sk[i] - skm1[i];
+        skm1[i] = sk[i];
+        sk[i] = sn;
+        p[i] = p[i] + ke * sk[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) p[i] = p[i] * kPi;
+  }
+  // exponent of the drift factor at each node (quadratic in g)
+  double cexp[5];
+  if (sv == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) cexp[i] = (((-v) * a) * g[i]) - (T.vvx * 0.5);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const double azsv = (a * g[i]) * sv;
+      cexp[i] = (((azsv * azsv) - (((2.0 * a) * v) * g[i])) - T.vvx) * T.cden;
+    }
+  }
+  double ex[5];
+  const bool moderate = fabs(cexp[0]) < 600.0 && fabs(cexp[2]) < 600.0 && fabs(cexp[4]) < 600.0;
+  if (moderate) {
+    // c_j = c0 + j d1 + j(j-1)/2 d2  ->  E_j = E_{j-1} * R * Q^(j-1)
+    const double d1 = cexp[1] - cexp[0];
+    const double d2 = (cexp[2] - cexp[1]) - d1;
+    ex[0] = exp(cexp[0]);
+    double rr = exp(d1);
+    const double qq = exp(d2);
+#pragma unroll
+    for (int j = 1; j < 5; ++j) {
+      ex[j] = ex[j - 1] * rr;
+      rr = rr * qq;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) ex[i] = exp(cexp[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    double r2 = (p[i] * ex[i]) * T.sc;
+    if (sv != 0 && p[i] < 0) r2 = __builtin_nan("");  // log(p < 0) in the reference
+    // exp(log 0 + c) = 0 even if e^c = inf; 0 * sc keeps the reference's
+    // 0 / (a*a) = NaN at a == 0
+    if (p[i] == 0) r2 = 0.0 * T.sc;
+    out[i] = r2;
+  }
+  // exp(c) overflow: the reference's literal exp(log p + c) (rare, per lane)
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+    if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, g[i], v, sv, a);
+}
+
 // Root-level adaptive Simpson over z at a fixed t node: 5 evaluations, run
-// 5-wide (tnode_pdf_sv_n) since they share the t node's branch and K.
+// 5-wide on the equally spaced grid (they share the t node's branch and K).
 __device__ inline double level0_z(const TNode& T, double lb, double ub, double iZT, double serr,
                                   int depth, double v, double sv, double a, bool& slow) {
   const double c = (ub + lb) / 2.;
-  const double w[5] = {lb, ub, c, (lb + c) / 2., (c + ub) / 2.};
+  const double g[5] = {lb, (lb + c) / 2., c, (c + ub) / 2., ub};  // lb, d, c, e, ub
   double f[5];
-  tnode_pdf_sv_n<5>(T, w, v, sv, a, f);
+  tnode_pdf_sv_grid5(T, g, v, sv, a, f);
 #pragma unroll
   for (int i = 0; i < 5; ++i) f[i] = f[i] * iZT;
+  // reference names: f_beg = f[0], f_end = f[4], f_mid = f[2], fd = f[1], fe = f[3]
   const double h = ub - lb;
-  const double S = (h / 6) * ((f[0] + (4 * f[2])) + f[1]);
-  const double Sl = (h / 12) * ((f[0] + (4 * f[3])) + f[2]);
-  const double Sr = (h / 12) * ((f[2] + (4 * f[4])) + f[1]);
+  const double S = (h / 6) * ((f[0] + (4 * f[2])) + f[4]);
+  const double Sl = (h / 12) * ((f[0] + (4 * f[1])) + f[2]);
+  const double Sr = (h / 12) * ((f[2] + (4 * f[3])) + f[4]);
   const double S2 = Sl + Sr;
   if (!(depth <= 0 || fabs(S2 - S) <= 15 * serr)) slow = true;
   return S2 + (S2 - S) / 15;
