@@ -68,6 +68,7 @@ wfpt_pdf_array = _sig("wfpt_pdf_array", _I, [_VP, _PD, _I64, _PP, _PK, _I, _PD])
 wfpt_full_pdf = _sig("wfpt_full_pdf", _I, [_VP, _D, _PP, _PK, _PD])
 wfpt_wiener_like_multi = _sig("wfpt_wiener_like_multi", _I,
                               [_VP, _PD, _I64, ctypes.POINTER(_PD), _PD, _PK, _D, _PD])
+wfpt_dmat_cdf_array = _sig("wfpt_dmat_cdf_array", _I, [_VP, _PD, _I64, _PP, _D, _PD])
 wfpt_comm_unique_id = _sig("wfpt_comm_unique_id", _I, [ctypes.c_char_p])
 wfpt_comm_init = _sig("wfpt_comm_init", _I, [_VP, _I, _I, ctypes.c_char_p])
 wfpt_wiener_like_allreduce = _sig("wfpt_wiener_like_allreduce", _I, [_VP, _VP, _PP, _PK, _PD])
@@ -80,7 +81,7 @@ EXPORTED = [
     "wfpt_device_count", "wfpt_open", "wfpt_close", "wfpt_last_error", "wfpt_dataset_create",
     "wfpt_dataset_destroy", "wfpt_dataset_size", "wfpt_shard_range", "wfpt_wiener_like",
     "wfpt_wiener_like_host", "wfpt_wiener_like_nodes", "wfpt_pdf_array", "wfpt_full_pdf",
-    "wfpt_wiener_like_multi", "wfpt_comm_unique_id", "wfpt_comm_init",
+    "wfpt_wiener_like_multi", "wfpt_dmat_cdf_array", "wfpt_comm_unique_id", "wfpt_comm_init",
     "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
 ]
 

@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libwfpt_amd.so")
-SOURCES = ["wfpt_kernels.hip", "wfpt_capi.cpp"]
+SOURCES = ["wfpt_kernels.hip", "cdfdif_kernels.hip", "wfpt_capi.cpp"]
 DEPS = SOURCES + ["wfpt_device.hpp", "wfpt_internal.h"]
 ARCH = os.environ.get("WFPT_OFFLOAD_ARCH", "gfx950")
 

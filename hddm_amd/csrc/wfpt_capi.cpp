@@ -539,6 +539,40 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   return WFPT_OK;
 }
 
+int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
+                        double w_outlier, double* out) {
+  if (!c || (!x && n > 0) || !p || (!out && n > 0) || n < 0)
+    return fail(WFPT_ERR_ARG, "bad arguments");
+  const double v = p->v, sv = p->sv, a = p->a, z = p->z, sz = p->sz, t = p->t, st = p->st;
+  const double po = p->p_outlier;
+  // cdfdif_wrapper.pyx:23-25
+  if ((sv < 0) || (a <= 0) || (z < 0) || (z > 1) || (sz < 0) || (sz > 1) || (z + sz / 2. > 1) ||
+      (z - sz / 2. < 0) || (t - st / 2. < 0) || (t < 0) || (st < 0) || !p_outlier_in_range(po))
+    return fail(WFPT_ERR_ARG, "at least one of the parameters is out of the support");
+  if (n == 0) return WFPT_OK;
+  // cdfdif_wrapper.pyx:35-42 (the model's units: a and z scaled by 1/10, s = 0.1)
+  const double epsi = 1e-10;
+  const double par[7] = {a / 10., t, sv / 10. + epsi, z * (a / 10.), sz * (a / 10.) + epsi,
+                         st + epsi, v / 10.};
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = upload(c, x, n)) return rc;
+  HIP_TRY(c->lp.reserve(n));
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  wfpt::launch_dmat_cdf(c->x.p, n, par, po, w_outlier, c->lp.p, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  HIP_TRY(hipMemcpyAsync(out, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->profile) {
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    c->k_ms += ms;
+    c->launches += 1;
+  }
+  return WFPT_OK;
+}
+
 int wfpt_comm_unique_id(unsigned char id[128]) {
   if (!id) return fail(WFPT_ERR_ARG, "null pointer");
   static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");

@@ -30,4 +30,8 @@ void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, d
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
                   const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
                   hipStream_t s);
+// cdfdif_kernels.hip: dmat_cdf_array over device x[n]; par = the wrapper's
+// transformed (a, Ter, eta, z, sZ, st, nu) (cdfdif_wrapper.pyx:36-42).
+void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
+                     double w_outlier, double* out, hipStream_t s);
 }  // namespace wfpt

@@ -16,6 +16,8 @@
  *   wfpt_wiener_like_nodes <- one wfpt_like per PyMC node, batched
  *                             hddm/likelihoods.py:52-73 via base.py:754-757
  *   wfpt_wiener_like_multi <- wfpt.wiener_like_multi   src/wfpt.pyx:244-274
+ *   wfpt_dmat_cdf_array    <- cdfdif_wrapper.dmat_cdf_array
+ *                             src/cdfdif_wrapper.pyx:16-53, src/cdfdif.c:59-221
  * The Python binding that keeps the reference signatures is
  * hddm_amd/wfpt.py (ctypes); INTEGRATION.md shows the drop-in.
  */
@@ -107,6 +109,15 @@ int wfpt_full_pdf(wfpt_ctx *ctx, double x, const wfpt_params *p, const wfpt_knob
 int wfpt_wiener_like_multi(wfpt_ctx *ctx, const double *x, int64_t n,
                            const double *const arrays[7], const double scalars[7],
                            const wfpt_knobs *k, double p_outlier, double *out_logp);
+
+/* ---- DMAT / Tuerlinckx CDF ---------------------------------------------- */
+/* Per-trial CDF of signed RTs with the outlier mixture, exactly
+ * cdfdif_wrapper.dmat_cdf_array(x, v, sv, a, z, sz, t, st, p_outlier, w_outlier)
+ * (src/cdfdif_wrapper.pyx:16-53 over cdfdif, src/cdfdif.c:59-221); p->p_outlier
+ * is the mixture weight. Parameters outside the support return WFPT_ERR_ARG
+ * (the reference raises ValueError, cdfdif_wrapper.pyx:23-25). */
+int wfpt_dmat_cdf_array(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
+                        double w_outlier, double *out);
 
 /* ---- multi-GPU (one process per GPU, RCCL over xGMI) -------------------- */
 /* 128-byte RCCL unique id, created on rank 0 and broadcast by the caller. */

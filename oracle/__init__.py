@@ -151,8 +151,7 @@ def count_evals(x, v, sv, a, z, sz, t, st, err=1e-4, n_st=2, n_sz=2, use_adaptiv
                                     int(use_adaptive), simps_err)
 
 
-def load_ref():
-    """Import oracle/_ref/ref_shim (the reference's own kernels) or return None."""
+def _load_ref_module(name):
     import importlib
     import sys
     d = os.path.join(HERE, "_ref")
@@ -161,6 +160,17 @@ def load_ref():
     if d not in sys.path:
         sys.path.insert(0, d)
     try:
-        return importlib.import_module("ref_shim")
+        return importlib.import_module(name)
     except ImportError:
         return None
+
+
+def load_ref():
+    """Import oracle/_ref/ref_shim (the reference's own kernels) or return None."""
+    return _load_ref_module("ref_shim")
+
+
+def load_ref_cdfdif():
+    """Import oracle/_ref/cdfdif_wrapper (the reference's own cdfdif_wrapper
+    extension, src/cdfdif_wrapper.pyx + src/cdfdif.c) or return None."""
+    return _load_ref_module("cdfdif_wrapper")

@@ -43,7 +43,35 @@ def build(reference="/root/reference", quiet=False):
     return so
 
 
+def build_cdfdif(reference="/root/reference", quiet=False):
+    """The reference's own `cdfdif_wrapper` extension (src/cdfdif_wrapper.pyx +
+    src/cdfdif.c, setup.py:9-13) compiled where the sources lie, into
+    oracle/_ref/cdfdif_wrapper<EXT_SUFFIX>. It imports nothing from hddm."""
+    src = os.path.join(reference, "src")
+    pyx = os.path.join(src, "cdfdif_wrapper.pyx")
+    csrc = os.path.join(src, "cdfdif.c")
+    if not os.path.isfile(pyx):
+        raise FileNotFoundError(f"reference sources not found under {src}")
+    import numpy as np
+    os.makedirs(OUT, exist_ok=True)
+    c = os.path.join(OUT, "cdfdif_wrapper.c")
+    so = os.path.join(OUT, "cdfdif_wrapper" + sysconfig.get_config_var("EXT_SUFFIX"))
+    if (os.path.exists(so) and os.path.getmtime(so) > os.path.getmtime(pyx)
+            and os.path.getmtime(so) > os.path.getmtime(csrc)):
+        return so
+    run = (lambda c_: subprocess.run(c_, check=True, stdout=subprocess.DEVNULL)) if quiet else \
+        (lambda c_: subprocess.run(c_, check=True))
+    run([sys.executable, "-m", "cython", "-2", "-I", src, "-o", c, pyx])
+    run(["gcc", "-O2", "-fwrapv", "-fPIC", "-DNDEBUG", "-shared",
+         "-DNPY_NO_DEPRECATED_API=NPY_1_7_API_VERSION",
+         "-I", src, "-I", sysconfig.get_paths()["include"], "-I", np.get_include(),
+         c, csrc, "-o", so, "-lm"])
+    return so
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
-    print(build(ap.parse_args().reference))
+    ref = ap.parse_args().reference
+    print(build(ref))
+    print(build_cdfdif(ref))

@@ -1,0 +1,111 @@
+"""DMAT / Tuerlinckx CDF (§8(f) row 4): hddm_amd.cdfdif_wrapper.dmat_cdf_array vs
+the reference's own `cdfdif_wrapper` (src/cdfdif_wrapper.pyx:16-53, src/cdfdif.c).
+
+Fixtures: tests/golden/cdfdif.npz, generated from the reference extension by
+tests/golden/make_golden_cdfdif.py. On the GPU box oracle/_ref (built here)
+also provides the reference for random inputs.
+
+Tolerance. The kernel keeps the reference's expression order; only libm vs
+OCML transcendental ulps differ. The reference evaluates F as a difference of
+terms divided by sZ*st (cdfdif.c:148, 206) and replaces sz = 0 / st = 0 by
+1e-10 (cdfdif_wrapper.pyx:38-41), which amplifies a 1-ulp difference by up
+to ~1e10 relative to the terms: the reference's own value is only that
+accurate there. The bar is therefore |dF| <= CDF_ATOL where sz and st are
+both >= 0.05 (well conditioned) and |dF| <= CDF_ATOL_ILL otherwise.
+"""
+import numpy as np
+import pytest
+
+CDF_ATOL = 1e-9
+CDF_ATOL_ILL = 1e-5
+
+
+def _golden():
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cdfdif.npz")
+    return dict(np.load(d, allow_pickle=False))
+
+
+def _tol(p):
+    return CDF_ATOL if (p[4] >= 0.05 and p[6] >= 0.05) else CDF_ATOL_ILL
+
+
+def test_golden_fixture_pinned_to_reference():
+    """The committed fixture equals the reference extension run here (when built)."""
+    import oracle
+    C = oracle.load_ref_cdfdif()
+    if C is None:
+        pytest.skip("oracle/_ref/cdfdif_wrapper not built")
+    g = _golden()
+    for p, x, y in zip(g["params"], g["x"], g["y"]):
+        np.testing.assert_array_equal(C.dmat_cdf_array(x, *p), y)
+
+
+def test_argument_semantics_match_reference():
+    """Checks that raise before any device work (cdfdif_wrapper.pyx:20-25, :11-12)."""
+    from hddm_amd import cdfdif_wrapper as cw
+    x = np.array([0.5, -0.7])
+    with pytest.raises(ValueError):
+        cw.dmat_cdf_array(x, 0.5, 0.0, 0.0, 0.5, 0.0, 0.3, 0.0, 0.0, 0.1)  # a <= 0
+    with pytest.raises(ValueError):
+        cw.dmat_cdf_array(x, 0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 1.5, 0.1)  # p_outlier
+    with pytest.raises(ValueError):
+        cw.dmat_cdf_array(x, 0.5, 0.0, 2.0, 0.9, 0.4, 0.3, 0.0, 0.0, 0.1)  # z + sz/2 > 1
+    with pytest.raises(AssertionError):
+        cw.dmat_cdf_array(np.array([6.0]), 0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 0.05, 0.1)
+    with pytest.raises(ValueError):  # np.max of an empty array
+        cw.dmat_cdf_array(np.zeros(0), 0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 0.05, 0.1)
+    with pytest.raises(ZeroDivisionError):
+        cw.dmat_cdf_array(x, 0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 0.0, 0.0)
+    with pytest.raises(TypeError):
+        cw.dmat_cdf_array([0.5], 0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 0.0, 0.1)
+    assert cw.dmat_cdf_array(np.zeros(0), 0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 0.0, 0.0).size == 0
+
+
+@pytest.mark.gpu
+def test_golden_cdfdif_parity():
+    from hddm_amd import cdfdif_wrapper as cw
+    g = _golden()
+    worst = 0.0
+    for p, x, y in zip(g["params"], g["x"], g["y"]):
+        got = cw.dmat_cdf_array(x, *p)
+        d = np.abs(got - y)
+        worst = max(worst, float(d.max()))
+        assert d.max() <= _tol(p), f"params {p}: max |dF| {d.max():.3e} at x={x[d.argmax()]}"
+    print(f"cdfdif golden: max |dF| = {worst:.3e}")
+
+
+@pytest.mark.gpu
+def test_random_cdfdif_vs_reference():
+    import oracle
+    from hddm_amd import cdfdif_wrapper as cw
+    C = oracle.load_ref_cdfdif()
+    if C is None:
+        pytest.skip("oracle/_ref/cdfdif_wrapper not built")
+    rng = np.random.default_rng(77)
+    for rep in range(10):
+        p = [rng.uniform(-3, 3), rng.choice([0.0, rng.uniform(0, 2)]), rng.uniform(0.6, 2.0),
+             rng.uniform(0.4, 0.6), rng.choice([0.0, rng.uniform(0.05, 0.3)]),
+             rng.uniform(0.2, 0.45), rng.choice([0.0, rng.uniform(0.05, 0.3)]),
+             rng.choice([0.0, 0.05]), 0.1]
+        x = rng.choice([-1.0, 1.0], 2000) * (p[5] - p[6] / 2 + rng.gamma(1.5, 0.5, 2000))
+        x = np.clip(x, -4.9, 4.9)
+        ref = C.dmat_cdf_array(x, *p)
+        got = cw.dmat_cdf_array(x, *p)
+        d = np.abs(got - ref)
+        assert d.max() <= _tol(p), f"params {p}: max |dF| {d.max():.3e}"
+
+
+@pytest.mark.gpu
+def test_cdfdif_properties():
+    """Size-independent properties: monotone in |rt| per boundary up to the
+    reference's own noise, limits P(lower) / 1 at |rt| -> inf."""
+    from hddm_amd import cdfdif_wrapper as cw
+    p = (0.5, 0.3, 2.0, 0.5, 0.2, 0.3, 0.1, 0.0, 0.1)
+    t = np.linspace(0.36, 30.0, 4000)
+    up = cw.dmat_cdf_array(t, *p)
+    lo = cw.dmat_cdf_array(-t, *p)
+    assert np.all(np.diff(up) >= -1e-9)
+    assert np.all(np.diff(lo) <= 1e-9)
+    assert abs(up[-1] - 1.0) < 1e-6
+    assert abs(lo[-1] - 0.0) < 1e-6
