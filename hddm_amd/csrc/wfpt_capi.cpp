@@ -2,7 +2,9 @@
 //
 // Host runtime: one context per GPU (HIP stream, grow-only device workspaces,
 // pinned result slot, optional RCCL communicator), resident datasets, and the
-// call sequences  trial kernel -> finalize -> 16-byte D2H  per likelihood.
+// call sequences  fast pass -> slow pass -> finalize  per likelihood; finalize
+// writes {sum, #zeros, status} straight into mapped pinned host memory, so a
+// resident-data call is three kernels and one stream sync (no copy, no memset).
 // Calls into one context are serialised by its mutex; the ctypes binding
 // releases the GIL around every call.
 #include <hip/hip_runtime.h>
@@ -82,6 +84,8 @@ struct wfpt_ctx {
   int* host_status = nullptr; // pinned mirror
   double* host = nullptr;  // pinned result slot
   size_t host_cap = 0;
+  double* mres = nullptr;      // mapped pinned {sum, zeros, status}: finalize writes it
+  double* mres_dev = nullptr;  // its device alias
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
   double k_ms = 0.0;
@@ -151,9 +155,8 @@ int ensure_host(wfpt_ctx* c, size_t n) {
   return WFPT_OK;
 }
 
-// Runs the trial kernel (block sums) + finalize on device x[n]; leaves
-// {sum, zeros} in c->res.p[0..1] (device). Records profile events.
-// Zero the overflow flag before a launch; check it after the stream sync.
+// Paths without finalize_kernel (pdf_array, nodes): clear the overflow flag
+// before the launch, copy it back (and clear it again) before the stream sync.
 int begin_status(wfpt_ctx* c) {
   HIP_TRY(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
   return WFPT_OK;
@@ -161,19 +164,11 @@ int begin_status(wfpt_ctx* c) {
 int fetch_status(wfpt_ctx* c) {
   HIP_TRY(hipMemcpyAsync(c->host_status, c->status, sizeof(int), hipMemcpyDeviceToHost,
                          c->stream));
+  HIP_TRY(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));  // 0 at rest
   return WFPT_OK;
 }
-int check_status(wfpt_ctx* c) {
-  const int st = *c->host_status;
-  if (st & 1)
-    return fail(WFPT_ERR_UNSUPPORTED,
-                "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
-                    std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)");
-  if (st & 2)
-    return fail(WFPT_ERR_UNSUPPORTED,
-                "a trial exceeded WFPT_EVAL_BUDGET pdf_sv evaluations (raise simps_err)");
-  return WFPT_OK;
-}
+int check_status_value(double st);
+int check_status(wfpt_ctx* c) { return check_status_value((double)(*c->host_status & 3)); }
 
 // Worklists: one byte per trial slot and one count per fast block; blocks own
 // 256 trials (1-D kernels) or 64 (outer-t split), so size for the finer one.
@@ -184,13 +179,29 @@ int reserve_worklist(wfpt_ctx* c, int64_t n) {
   return WFPT_OK;
 }
 
+// Status words are 0 at rest: finalize_kernel resets the device flag after
+// reporting it, and the other paths clear it before their launch.
+int check_status_value(double st) {
+  const int s = (int)st;
+  if (s == 0) return WFPT_OK;
+  if (s == 1)
+    return fail(WFPT_ERR_UNSUPPORTED,
+                "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
+                    std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)");
+  if (s == 2)
+    return fail(WFPT_ERR_UNSUPPORTED,
+                "a trial exceeded WFPT_EVAL_BUDGET pdf_sv evaluations (raise simps_err)");
+  return fail(WFPT_ERR_UNSUPPORTED, "Simpson depth / evaluation budget exceeded (status " +
+                                        std::to_string(s) + ", summed over ranks)");
+}
+
+// Fast pass (+ slow pass) + finalize over device x[n]; the 3-double result
+// {sum, zeros, status} lands in `out` (mapped host memory or device).
 int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
-            const wfpt::Knobs& K) {
+            const wfpt::Knobs& K, double* out) {
   const int64_t nb = wfpt::partials_for(n, P, K);
-  if (int rc = begin_status(c)) return rc;
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
-  HIP_TRY(c->res.reserve(2));
   if (int rc = reserve_worklist(c, n)) return rc;
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
@@ -198,12 +209,8 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
                       c->status, 0, c->wl.p, c->wl_n.p, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  if (nb > 0) {
-    wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->res.p, c->stream);
-    HIP_TRY(hipGetLastError());
-  } else {
-    HIP_TRY(hipMemsetAsync(c->res.p, 0, 2 * sizeof(double), c->stream));
-  }
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, out, c->stream);
+  HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
 
@@ -222,17 +229,12 @@ int finish_profile(wfpt_ctx* c) {
   return WFPT_OK;
 }
 
-int read_sum(wfpt_ctx* c, double* out) {
-  int rc = ensure_host(c, 2);
-  if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, 2 * sizeof(double), hipMemcpyDeviceToHost,
-                         c->stream));
-  if ((rc = fetch_status(c))) return rc;
+// Waits for the call and decodes {sum, zeros, status} from host memory `r`.
+int read_sum(wfpt_ctx* c, const double* r, double* out) {
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if ((rc = check_status(c))) return rc;
-  rc = finish_profile(c);
-  if (rc) return rc;
-  *out = (c->host[1] > 0) ? -INFINITY : c->host[0];
+  if (int rc = check_status_value(r[2])) return rc;
+  if (int rc = finish_profile(c)) return rc;
+  *out = (r[1] > 0) ? -INFINITY : r[0];
   return WFPT_OK;
 }
 
@@ -272,6 +274,11 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipMalloc((void**)&c->evals, sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMalloc((void**)&c->status, sizeof(int));
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->host_status, sizeof(int), hipHostMallocDefault);
+  if (e == hipSuccess) e = hipMemset(c->status, 0, sizeof(int));
+  if (e == hipSuccess)
+    e = hipHostMalloc((void**)&c->mres, 4 * sizeof(double),
+                      hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e != hipSuccess) {
     wfpt_close(c);
     return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
@@ -300,6 +307,7 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
   if (c->host) (void)hipHostFree(c->host);
+  if (c->mres) (void)hipHostFree(c->mres);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -397,8 +405,8 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  if (int rc = run_sum(c, d->x, d->n, P, K)) return rc;
-  return read_sum(c, out);
+  if (int rc = run_sum(c, d->x, d->n, P, K, c->mres_dev)) return rc;
+  return read_sum(c, c->mres, out);
 }
 
 int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
@@ -413,8 +421,8 @@ int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_pa
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   if (int rc = upload(c, x, n)) return rc;
-  if (int rc = run_sum(c, c->x.p, n, P, K)) return rc;
-  return read_sum(c, out);
+  if (int rc = run_sum(c, c->x.p, n, P, K, c->mres_dev)) return rc;
+  return read_sum(c, c->mres, out);
 }
 
 int wfpt_pdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
@@ -518,24 +526,14 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   const int64_t nb = wfpt::blocks_for(n);
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
-  HIP_TRY(c->res.reserve(2));
-  if (int rc = begin_status(c)) return rc;
   wfpt::launch_multi(c->x.p, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
                      c->status, c->stream);
   HIP_TRY(hipGetLastError());
-  if (nb > 0) {
-    wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->res.p, c->stream);
-    HIP_TRY(hipGetLastError());
-  } else {
-    HIP_TRY(hipMemsetAsync(c->res.p, 0, 2 * sizeof(double), c->stream));
-  }
-  if (int rc = ensure_host(c, 2)) return rc;
-  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, 2 * sizeof(double), hipMemcpyDeviceToHost,
-                         c->stream));
-  if (int rc = fetch_status(c)) return rc;
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, c->mres_dev, c->stream);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if (int rc = check_status(c)) return rc;
-  *out = c->host[0];
+  if (int rc = check_status_value(c->mres[2])) return rc;
+  *out = c->mres[0];
   return WFPT_OK;
 }
 
@@ -612,9 +610,15 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  if (int rc = run_sum(c, d->x, d->n, P, K)) return rc;
-  NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 2, ncclDouble, ncclSum, c->comm, c->stream));
-  return read_sum(c, out);
+  HIP_TRY(c->res.reserve(3));
+  if (int rc = ensure_host(c, 3)) return rc;
+  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p)) return rc;
+  // {sum, zeros, status} of every rank summed: any zero trial or failure anywhere
+  // reaches every rank
+  NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 3, ncclDouble, ncclSum, c->comm, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, 3 * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream));
+  return read_sum(c, c->host, out);
 }
 
 int wfpt_profile_enable(wfpt_ctx* c, int flags) {

@@ -250,68 +250,85 @@ __global__ WFPT_FAST_T_BOUNDS void fast_t_kernel(TrialArgs A, unsigned char* wl,
   }
 }
 
-// General pass over the trials the fast pass deferred: block b runs the
-// wl_n[b] slow trials of fast block b on its first wl_n[b] lanes (full
-// adaptive quadrature, reference recursion order). OUT_SUM partials go to
-// A.out[nb + b] / A.zeros[nb + b] so the finalize sum stays in fixed order.
-template <int MODE, int STK, bool COUNT, int OUT, int TPB>
-__global__ __launch_bounds__(TPB) void slow_kernel(TrialArgs A, const unsigned char* wl,
-                                                   const int* wl_n, int64_t nb) {
+// General pass over the trials the fast pass deferred. The fast pass leaves
+// one worklist per 64 trials (nl lists); this one-wave-per-block kernel runs
+// on a bounded grid (kSlowGrid blocks) and block g walks lists g, g + G, ...,
+// running the wl_n[b] deferred trials of list b on its first lanes (full
+// adaptive quadrature, reference recursion order). An empty list costs one
+// scalar load, so a workload with (almost) nothing deferred pays a short
+// launch, not one block per 64 trials. OUT_SUM partials go to
+// A.out[nb + g] / A.zeros[nb + g]: each lane sums its own trials in list
+// order, then the wave tree, so the total is deterministic for a given n.
+constexpr int64_t kSlowGrid = 4096;
+
+template <int MODE, int STK, bool COUNT, int OUT>
+__global__ __launch_bounds__(64) void slow_kernel(TrialArgs A, const unsigned char* wl,
+                                                  const int* wl_n, int64_t nl, int64_t nb) {
   using Stack = typename StackOf<STK>::type;
-  const int cnt = wl_n[blockIdx.x];
-  if (cnt == 0) {
-    if (OUT == OUT_SUM && threadIdx.x == 0) {
-      A.out[nb + blockIdx.x] = 0.0;
-      A.zeros[nb + blockIdx.x] = 0;
-    }
-    return;
-  }
   long long ne = 0;
   double lp = 0.0;
-  int zero = 0, ovf = 0;
-  if ((int)threadIdx.x < cnt) {
-    const int64_t i = (int64_t)blockIdx.x * TPB + wl[(int64_t)blockIdx.x * TPB + threadIdx.x];
+  long long zc = 0;
+  int ovf = 0;
+  for (int64_t b = blockIdx.x; b < nl; b += gridDim.x) {
+    const int cnt = wl_n[b];
+    if ((int)threadIdx.x >= cnt) continue;
+    const int64_t i = b * 64 + wl[b * 64 + threadIdx.x];
     double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
-    if (ovf) atomicOr(A.status, ovf);
     if (OUT == OUT_ARRAY) {
       p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);
       A.out[i] = A.logp ? log(p) : p;
     } else {
       p = p * (1 - A.P.p_outlier) + A.wp_outlier;
-      if (p == 0) zero = 1;
-      else lp = log(p);
-      if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+      const bool z = p == 0;
+      double l = 0.0;
+      if (z) zc += 1;
+      else l = log(p);
+      lp += l;
+      if (OUT == OUT_LOGP) A.out[i] = z ? -INFINITY : l;
     }
   }
+  if (ovf) atomicOr(A.status, ovf);
   if (OUT == OUT_SUM || COUNT) {
-    if (TPB == kBlock) {
-      block_reduce<COUNT>(lp, zero, ne);
-    } else {  // one wave
-      lp = wave_sum(lp);
-      zero = __popcll(__ballot(zero != 0));
-      if (COUNT) ne = wave_sum_ll(ne);
-    }
+    lp = wave_sum(lp);
+    zc = wave_sum_ll(zc);
+    if (COUNT) ne = wave_sum_ll(ne);
     if (threadIdx.x == 0) {
       if (OUT == OUT_SUM) {
         A.out[nb + blockIdx.x] = lp;
-        A.zeros[nb + blockIdx.x] = zero;
+        A.zeros[nb + blockIdx.x] = (int)zc;
       }
       if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
     }
   }
 }
 
-// out[0] = sum of partials, out[1] = number of zero trials (as double).
+__host__ __device__ inline int64_t slow_grid(int64_t nl) { return nl < kSlowGrid ? nl : kSlowGrid; }
+
+// out[0] = sum of partials, out[1] = number of zero trials, out[2] = the
+// call's status flags (as doubles); the device status word is reset to 0 for
+// the next call. `out` may be mapped pinned host memory: the 24-byte result
+// then reaches the host with the kernel, without a copy. Fixed summation
+// order for a given nb (4 independent accumulators per thread keep 4 loads
+// in flight).
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
-                                                        int64_t nb, double* out) {
+                                                        int64_t nb, int* status, double* out) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
-  double s = 0.0;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   long long z = 0;
-  for (int64_t b = threadIdx.x; b < nb; b += 1024) {
-    s += part[b];
+  int64_t b = threadIdx.x;
+  for (; b + 3 * 1024 < nb; b += 4 * 1024) {
+    s0 += part[b];
+    s1 += part[b + 1024];
+    s2 += part[b + 2048];
+    s3 += part[b + 3072];
+    z += (long long)zeros[b] + zeros[b + 1024] + zeros[b + 2048] + zeros[b + 3072];
+  }
+  for (; b < nb; b += 1024) {
+    s0 += part[b];
     z += zeros[b];
   }
+  double s = (s0 + s1) + (s2 + s3);
   s = wave_sum(s);
   z = wave_sum_ll(z);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -327,8 +344,12 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
       t += ss[k];
       zz += sz[k];
     }
+    const int st = *status;
+    *status = 0;
     out[0] = t;
     out[1] = (double)zz;
+    out[2] = (double)st;
+    __threadfence_system();
   }
 }
 
@@ -458,15 +479,16 @@ static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned cha
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
                        A, wl, wl_n);
   if (MODE == kDirect) return;
+  const int64_t g = slow_grid(nb);
   if (stk == 0)
-    hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
-                       wl_n, nb);
+    hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT>), dim3(g), dim3(TPB), 0, s, A, wl, wl_n,
+                       nb, nb);
   else if (stk == 1)
-    hipLaunchKernelGGL((slow_kernel<MODE, 1, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
-                       wl_n, nb);
+    hipLaunchKernelGGL((slow_kernel<MODE, 1, COUNT, OUT>), dim3(g), dim3(TPB), 0, s, A, wl, wl_n,
+                       nb, nb);
   else
-    hipLaunchKernelGGL((slow_kernel<MODE, 2, COUNT, OUT, TPB>), dim3(nb), dim3(TPB), 0, s, A, wl,
-                       wl_n, nb);
+    hipLaunchKernelGGL((slow_kernel<MODE, 2, COUNT, OUT>), dim3(g), dim3(TPB), 0, s, A, wl, wl_n,
+                       nb, nb);
 }
 
 template <bool COUNT, int OUT>
@@ -495,7 +517,7 @@ static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, in
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   const int64_t nw = (n + 63) / 64;  // fast (and slow) partials are per 64 trials
-  if (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) return 2 * nw;
+  if (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) return nw + slow_grid(nw);
   if (mode == kDirect) return nw;
   return blocks_for(n);  // fixed Simpson: trial_kernel, one partial per 256-trial block
 }
@@ -528,9 +550,9 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
   else launch_count<false>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s);
 }
 
-void launch_finalize(const double* part, const int* zeros, int64_t nb, double* out,
+void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
                      hipStream_t s) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, out);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, status, out);
 }
 
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
