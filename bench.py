@@ -75,18 +75,19 @@ def cpu_baseline(x, budget_s):
 
 
 def load_traffic(n_trials):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary, if present."""
+    """HBM bytes per launch and VALU issue utilisation of the main kernel from
+    the committed rocprofv3 PMC summary (profiles/traffic.json), if present."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as fh:
             t = json.load(fh)
         if int(t.get("n_trials", -1)) == int(n_trials):
-            return float(t["hbm_bytes_per_launch"])
+            return float(t["hbm_bytes_per_launch"]), t.get("valu_issue_utilisation")
     except Exception:
-        return None
-    return None
+        return None, None
+    return None, None
 
 
 def main():
@@ -137,8 +138,7 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
-    ctx.profile(ctx.PROF_EVENTS)
-    ctx.profile_read(reset=True)
+    # timed region: K plain calls (no per-launch instrumentation in the way)
     barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -147,6 +147,13 @@ def main():
     ctx.synchronize()
     barrier()
     el = time.perf_counter() - t0
+    # the same K calls again with HIP events recorded on the library's stream
+    # around the likelihood kernels of every call: per-launch kernel time
+    ctx.profile(ctx.PROF_EVENTS)
+    ctx.profile_read(reset=True)
+    for _ in range(a.steps):
+        step()
+    ctx.synchronize()
     k_ms, launches, _ = ctx.profile_read(reset=True)
     ctx.profile(0)
     if world > 1:
@@ -162,7 +169,7 @@ def main():
     w_trial = evals_per_trial * W_EVAL + W_EPI
     k_avg_s = (k_ms / 1e3) / max(launches, 1)
     achieved = n * w_trial / k_avg_s / 1e12
-    traffic = load_traffic(n)
+    traffic, valu_util = load_traffic(n)
     out = {
         "metric": METRIC,
         "value": value,
@@ -189,7 +196,10 @@ def main():
                      "unit": "T fp64-lane-ops/s", "frac": achieved / (PEAK_LANE_OPS / 1e12),
                      "traffic": traffic,
                      "kernel_ms_avg": k_avg_s * 1e3, "kernel_launches": launches,
-                     "w_trial_lane_ops": w_trial},
+                     "w_trial_lane_ops": w_trial,
+                     # hardware view (rocprofv3 PMC, profiles/traffic.json): share of SIMD
+                     # cycles issuing VALU (4 cycles per wave64 fp64 op, 2 otherwise)
+                     "valu_issue_utilisation": valu_util},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(x, a.cpu_seconds)

@@ -13,12 +13,14 @@ Restates hddm/likelihoods.py:30-105 (`generate_wfpt_stochastic_class`,
 * `generate_wfpt_stochastic_class` returns the same PyMC class as the
   reference when kabuki is importable (kabuki.utils.stochastic_from_dist);
   otherwise a light `WfptNode` with `.value`, `.parents`, `.logp`, `.pdf`,
-  `.random` so hierarchical samplers (hddm_amd.hierarchical) can drive it.
+  `.cdf`, `.random` so hierarchical samplers (hddm_amd.hierarchical) can drive it.
+  `.cdf` is the DMAT CDF (likelihoods.py:90-91 -> cdfdif_wrapper.dmat_cdf_array).
 """
 
 import numpy as np
 from scipy import stats
 
+from . import cdfdif_wrapper as _cdfdif
 from . import wfpt as _wfpt
 
 DEFAULT_WIENER_PARAMS = {"err": 1e-4, "n_st": 2, "n_sz": 2, "use_adaptive": 1,
@@ -112,6 +114,12 @@ class WfptNode:
                                pv["a"], pv["z"], pv["sz"], pv["t"], pv["st"],
                                p_outlier=pv["p_outlier"])
 
+    def cdf(self, x):
+        """likelihoods.py:90-91: DMAT CDF with the class's w_outlier."""
+        pv = self.parent_values()
+        return _cdfdif.dmat_cdf_array(np.ascontiguousarray(x, dtype=np.float64),
+                                      w_outlier=self._like.wiener_params["w_outlier"], **pv)
+
     def random(self, size=None):
         pv = self.parent_values()
         n = size or len(_rt_column(self.value))
@@ -140,5 +148,10 @@ def generate_wfpt_stochastic_class(wiener_params=None, sampling_method="cdf",
     def pdf(self, x):
         return _wfpt.pdf_array(x, **self.parents)
 
+    def cdf(self, x):
+        return _cdfdif.dmat_cdf_array(x, w_outlier=wfpt_like.wiener_params["w_outlier"],
+                                      **self.parents)
+
     wfpt_cls.pdf = pdf
+    wfpt_cls.cdf = cdf
     return wfpt_cls

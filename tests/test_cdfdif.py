@@ -11,13 +11,14 @@ terms divided by sZ*st (cdfdif.c:148, 206) and replaces sz = 0 / st = 0 by
 1e-10 (cdfdif_wrapper.pyx:38-41), which amplifies a 1-ulp difference by up
 to ~1e10 relative to the terms: the reference's own value is only that
 accurate there. The bar is therefore |dF| <= CDF_ATOL where sz and st are
-both >= 0.05 (well conditioned) and |dF| <= CDF_ATOL_ILL otherwise.
+both >= 0.05 (well conditioned) and |dF| <= CDF_ATOL_ILL otherwise
+(measured on MI355X: max |dF| = 1.4e-8 over the golden set).
 """
 import numpy as np
 import pytest
 
 CDF_ATOL = 1e-9
-CDF_ATOL_ILL = 1e-5
+CDF_ATOL_ILL = 1e-6
 
 
 def _golden():
@@ -109,3 +110,19 @@ def test_cdfdif_properties():
     assert np.all(np.diff(lo) <= 1e-9)
     assert abs(up[-1] - 1.0) < 1e-6
     assert abs(lo[-1] - 0.0) < 1e-6
+
+
+@pytest.mark.gpu
+def test_stochastic_cdf_hook():
+    """The node's `cdf` (likelihoods.py:90-91) is dmat_cdf_array with the class's w_outlier."""
+    import oracle
+    from hddm_amd.likelihoods import generate_wfpt_stochastic_class
+    C = oracle.load_ref_cdfdif()
+    if C is None:
+        pytest.skip("oracle/_ref/cdfdif_wrapper not built")
+    cls = generate_wfpt_stochastic_class()
+    node = cls("wfpt", np.array([0.5, -0.8]), v=0.7, sv=0.2, a=1.8, z=0.5, sz=0.1, t=0.3,
+               st=0.1, p_outlier=0.05)
+    x = np.linspace(-3, 3, 101)
+    np.testing.assert_allclose(node.cdf(x), C.dmat_cdf_array(x, 0.7, 0.2, 1.8, 0.5, 0.1, 0.3,
+                                                             0.1, 0.05, 0.1), atol=CDF_ATOL)
