@@ -694,18 +694,56 @@ __device__ inline double full_pdf(double x, const Params& P, const Knobs& K, lon
 // any root test asks for refinement; such trials are recomputed by the
 // general kernel (full_pdf above). MODE: kDirect, kAdaptT, kAdaptZ, kAdaptTZ.
 
-// pdf_sv at the 5 root-level z nodes of one t node, ordered as the equally
-// spaced grid g_j = lb + j (ub - lb) / 4, j = 0..4 (lb, d, c, e, ub). Same
-// values as tnode_pdf_sv_n<5> to a few ulp, using the grid structure:
-//   * large-t: sin/cos(pi g_j) for j = 1..3 by angle-addition rotation from
-//     the directly evaluated g_0; g_4 = ub is evaluated directly so the
-//     w = 1 edge keeps the reference's own sin(pi) value;
-//   * the sv factor exp(c(g_j)), c quadratic in g: 3 exponentials and the
-//     second-difference recurrence (direct exps when |c| > 600).
-// g[] holds the reference's own node coordinates (used for every polynomial
-// in w); only the transcendental factors use the recurrences.
-__device__ inline void tnode_pdf_sv_grid5(const TNode& T, const double (&g)[5], double v,
-                                          double sv, double a, double (&out)[5]) {
+// Per-trial part of the root-level z grid. The 5 z nodes (lb, d, c, e, ub of
+// integrate.pxi:114-141 / 143-178) are the same for every t node of a trial,
+// so everything that depends on z alone is computed once per trial:
+//   * sin/cos(pi g_0), sin/cos(pi g_4) and sin/cos(pi (g_4 - g_0) / 4), from
+//     which each large-time t node rotates to g_1..g_3 (angle addition); g_4 is
+//     evaluated directly so the w = 1 edge keeps the reference's sin(pi);
+//   * the z-only part A_j of the drift-factor exponent (pdf.pxi:96-101):
+//     c_j = (A_j - v^2 x) / (2 sv^2 x + 2)   (sv > 0),  c_j = A_j - v^2 x / 2  (sv = 0).
+// g[] holds the reference's own node coordinates (every polynomial in w uses
+// them); only transcendental factors use the rotations / recurrences.
+struct ZGrid {
+  double g[5];
+  double s0, c0, s4, c4, sd, cd;
+  double A[5];
+};
+
+__device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, double a) {
+  ZGrid G;
+  const double c = (ub + lb) / 2.;
+  G.g[0] = lb;
+  G.g[1] = (lb + c) / 2.;
+  G.g[2] = c;
+  G.g[3] = (c + ub) / 2.;
+  G.g[4] = ub;
+  sincospi01(G.g[0], G.s0, G.c0);
+  sincospi01(G.g[4], G.s4, G.c4);
+  sincospi01((G.g[4] - G.g[0]) * 0.25, G.sd, G.cd);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    if (sv == 0) {
+      G.A[i] = ((-v) * a) * G.g[i];
+    } else {
+      const double azsv = (a * G.g[i]) * sv;
+      G.A[i] = (azsv * azsv) - (((2.0 * a) * v) * G.g[i]);
+    }
+  }
+  return G;
+}
+
+// pdf_sv at the 5 root-level z nodes of one t node (same values as
+// tnode_pdf_sv_n<5> to a few ulp):
+//   * small-t series: the exponents (g_j + 2k)^2 m are quadratic in j on the
+//     equally spaced grid, so per term k two exponentials (j = 0 and the first
+//     ratio) and one shared second-difference factor replace five; exponents
+//     below -600 (subnormal territory) take the direct exps;
+//   * large-t series: the Chebyshev recurrence in k from the rotated sin/cos;
+//   * the drift factor exp(c_j): three exponentials and the second-difference
+//     recurrence (direct exps when |c| > 600).
+__device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
+                                          double a, double (&out)[5]) {
   double p[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) p[i] = 0.0;
@@ -718,26 +756,47 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const double (&g)[5], 
   if (T.small) {
     const int lower = (int)(-floor((K - 1) / 2.));
     const int upper = (int)ceil((K - 1) / 2.);
+    double qq = 0.0;
+    bool have_q = false;
     for (int k = lower; k <= upper; ++k) {
       const double k2 = (double)(2 * k);
+      double wk[5], ek[5];
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const double wk = g[i] + k2;
-        p[i] = p[i] + wk * exp((wk * wk) * T.m);
+        wk[i] = G.g[i] + k2;
+        ek[i] = (wk[i] * wk[i]) * T.m;
+      }
+      if (ek[0] > -600.0 && ek[4] > -600.0) {  // ek <= 0 and convex in j: ends are the minima
+        const double d1 = ek[1] - ek[0];
+        if (!have_q) {
+          qq = exp((ek[2] - ek[1]) - d1);
+          have_q = true;
+        }
+        double E = exp(ek[0]);
+        double R = exp(d1);
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+          p[i] = p[i] + wk[i] * E;
+          E = E * R;
+          R = R * qq;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) p[i] = p[i] + wk[i] * exp(ek[i]);
       }
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = p[i] * T.rn;
   } else {
     double sj[5], cj[5];
-    sincospi01(g[0], sj[0], cj[0]);
-    sincospi01(g[4], sj[4], cj[4]);
-    double sd, cd;
-    sincospi01((g[4] - g[0]) * 0.25, sd, cd);
+    sj[0] = G.s0;
+    cj[0] = G.c0;
+    sj[4] = G.s4;
+    cj[4] = G.c4;
 #pragma unroll
     for (int j = 1; j < 4; ++j) {
-      sj[j] = fma(sj[j - 1], cd, cj[j - 1] * sd);
-      cj[j] = fma(cj[j - 1], cd, -(sj[j - 1] * sd));
+      sj[j] = fma(sj[j - 1], G.cd, cj[j - 1] * G.sd);
+      cj[j] = fma(cj[j - 1], G.cd, -(sj[j - 1] * G.sd));
     }
     double tc[5], sk[5], skm1[5];
 #pragma unroll
@@ -765,16 +824,9 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const double (&g)[5], 
   }
   // exponent of the drift factor at each node (quadratic in g)
   double cexp[5];
-  if (sv == 0) {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) cexp[i] = (((-v) * a) * g[i]) - (T.vvx * 0.5);
-  } else {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      const double azsv = (a * g[i]) * sv;
-      cexp[i] = (((azsv * azsv) - (((2.0 * a) * v) * g[i])) - T.vvx) * T.cden;
-    }
-  }
+  for (int i = 0; i < 5; ++i)
+    cexp[i] = (sv == 0) ? G.A[i] - (T.vvx * 0.5) : (G.A[i] - T.vvx) * T.cden;
   double ex[5];
   const bool moderate = fabs(cexp[0]) < 600.0 && fabs(cexp[2]) < 600.0 && fabs(cexp[4]) < 600.0;
   if (moderate) {
@@ -783,11 +835,11 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const double (&g)[5], 
     const double d2 = (cexp[2] - cexp[1]) - d1;
     ex[0] = exp(cexp[0]);
     double rr = exp(d1);
-    const double qq = exp(d2);
+    const double qd = exp(d2);
 #pragma unroll
     for (int j = 1; j < 5; ++j) {
       ex[j] = ex[j - 1] * rr;
-      rr = rr * qq;
+      rr = rr * qd;
     }
   } else {
 #pragma unroll
@@ -805,21 +857,19 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const double (&g)[5], 
   // exp(c) overflow: the reference's literal exp(log p + c) (rare, per lane)
 #pragma unroll
   for (int i = 0; i < 5; ++i)
-    if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, g[i], v, sv, a);
+    if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, G.g[i], v, sv, a);
 }
 
 // Root-level adaptive Simpson over z at a fixed t node: 5 evaluations, run
 // 5-wide on the equally spaced grid (they share the t node's branch and K).
-__device__ inline double level0_z(const TNode& T, double lb, double ub, double iZT, double serr,
+__device__ inline double level0_z(const TNode& T, const ZGrid& G, double iZT, double serr,
                                   int depth, double v, double sv, double a, bool& slow) {
-  const double c = (ub + lb) / 2.;
-  const double g[5] = {lb, (lb + c) / 2., c, (c + ub) / 2., ub};  // lb, d, c, e, ub
   double f[5];
-  tnode_pdf_sv_grid5(T, g, v, sv, a, f);
+  tnode_pdf_sv_grid5(T, G, v, sv, a, f);
 #pragma unroll
   for (int i = 0; i < 5; ++i) f[i] = f[i] * iZT;
   // reference names: f_beg = f[0], f_end = f[4], f_mid = f[2], fd = f[1], fe = f[3]
-  const double h = ub - lb;
+  const double h = G.g[4] - G.g[0];
   const double S = (h / 6) * ((f[0] + (4 * f[2])) + f[4]);
   const double Sl = (h / 12) * ((f[0] + (4 * f[1])) + f[2]);
   const double Sr = (h / 12) * ((f[2] + (4 * f[3])) + f[4]);
@@ -851,8 +901,9 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
   if (MODE == kDirect) return pdf_sv(x - t, v, sv, a, z, err);
   if (MODE == kAdaptZ) {
     const double lb = z - sz / 2., ub = z + sz / 2.;
+    const ZGrid G = zgrid_setup(lb, ub, v, sv, a);
     const TNode T = tnode_setup(x - t, v, sv, a, err);
-    return level0_z(T, lb, ub, 1.0 / (ub - lb), K.simps_err, K.n_sz, v, sv, a, slow);
+    return level0_z(T, G, 1.0 / (ub - lb), K.simps_err, K.n_sz, v, sv, a, slow);
   }
   // t outer: kAdaptT (one evaluation per t node) or kAdaptTZ (a z integral per t node)
   const double lb = t - st / 2., ub = t + st / 2.;
@@ -861,6 +912,8 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
   const double lbz = z - sz / 2., ubz = z + sz / 2.;
   const double iZz = (MODE == kAdaptTZ) ? 1.0 / (ubz - lbz) : 0.0;
   const double iZt = 1.0 / (ub - lb);
+  ZGrid G;
+  if (MODE == kAdaptTZ) G = zgrid_setup(lbz, ubz, v, sv, a);
   double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
 #pragma unroll 1
   for (int j = 0; j < 5; ++j) {
@@ -868,7 +921,7 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
     const TNode T = tnode_setup(x - tc, v, sv, a, err);
     double y;
     if (MODE == kAdaptTZ) {
-      y = level0_z(T, lbz, ubz, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
+      y = level0_z(T, G, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
       if (slow) return 0.0;
     } else {
       y = tnode_pdf_sv(T, z, v, sv, a) * iZt;
@@ -928,8 +981,8 @@ __device__ inline double fast_t_node(const TrialPrep& R, int j, const Params& P,
   const TNode T = tnode_setup(R.x - tc, R.v, sv, a, K.err);
   if (MODE == kAdaptTZ) {
     const double lbz = R.z - R.sz / 2., ubz = R.z + R.sz / 2.;
-    return level0_z(T, lbz, ubz, 1.0 / (ubz - lbz), K.simps_err, K.n_sz, R.v, sv, a, slow) *
-           iZt;
+    const ZGrid G = zgrid_setup(lbz, ubz, R.v, sv, a);
+    return level0_z(T, G, 1.0 / (ubz - lbz), K.simps_err, K.n_sz, R.v, sv, a, slow) * iZt;
   }
   return tnode_pdf_sv(T, R.z, R.v, sv, a) * iZt;
 }

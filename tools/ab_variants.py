@@ -69,10 +69,11 @@ def build():
         print("built", name, flush=True)
 
 
-def run(reps):
-    out = {k: [] for k in VARIANTS}
+def run(reps, names=None):
+    names = names or list(VARIANTS)
+    out = {k: [] for k in names}
     for r in range(reps):
-        for name in VARIANTS:
+        for name in names:
             env = dict(os.environ, WFPT_AMD_LIB=os.path.join(LIBDIR, f"libwfpt_{name}.so"),
                        ROOT=ROOT)
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True,
@@ -97,4 +98,7 @@ if __name__ == "__main__":
         build()
     else:
         reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
-        sys.exit(run(reps))
+        # --names a,b: time already-built hddm_amd/lib/variants/libwfpt_<name>.so
+        names = (sys.argv[sys.argv.index("--names") + 1].split(",") if "--names" in sys.argv
+                 else None)
+        sys.exit(run(reps, names))
