@@ -11,6 +11,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -86,6 +88,8 @@ struct wfpt_ctx {
   size_t host_cap = 0;
   double* mres = nullptr;      // mapped pinned {sum, zeros, status}: finalize writes it
   double* mres_dev = nullptr;  // its device alias
+  unsigned long long seq = 0;  // completion word finalize writes to mres[3]
+  bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
   double k_ms = 0.0;
@@ -209,7 +213,10 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
                       c->status, 0, c->wl.p, c->wl_n.p, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, out, c->stream);
+  int64_t off = 0, cnt = 0;
+  wfpt::final_partials(n, P, K, &off, &cnt);
+  wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, out, ++c->seq,
+                        c->stream);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -229,9 +236,37 @@ int finish_profile(wfpt_ctx* c) {
   return WFPT_OK;
 }
 
+// Waits for the result of the last run_sum. For the mapped slot the host polls
+// the completion word finalize writes after the results (a stream sync's
+// wake-up costs several microseconds per call); every 4096 polls it asks the
+// stream whether it failed, and after 5 s it falls back to a stream sync so a
+// device error is reported, never a stale number.
+int wait_result(wfpt_ctx* c, const double* r) {
+  if (r == c->mres && c->spin) {
+    const volatile unsigned long long* w = reinterpret_cast<const volatile unsigned long long*>(r);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned it = 1;; ++it) {
+      if (w[3] == c->seq) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (c->profile) HIP_TRY(hipEventSynchronize(c->ev1));
+        return WFPT_OK;
+      }
+      if ((it & 4095u) == 0) {
+        const hipError_t q = hipStreamQuery(c->stream);
+        if (q != hipSuccess && q != hipErrorNotReady)
+          return fail(WFPT_ERR_HIP, std::string("likelihood kernels: ") + hipGetErrorString(q));
+        if (q == hipSuccess && w[3] != c->seq) break;  // idle: let the stream sync decide
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
+      }
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return WFPT_OK;
+}
+
 // Waits for the call and decodes {sum, zeros, status} from host memory `r`.
 int read_sum(wfpt_ctx* c, const double* r, double* out) {
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int rc = wait_result(c, r)) return rc;
   if (int rc = check_status_value(r[2])) return rc;
   if (int rc = finish_profile(c)) return rc;
   *out = (r[1] > 0) ? -INFINITY : r[0];
@@ -268,6 +303,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   auto* c = new wfpt_ctx();
   c->device = device;
+  if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -529,7 +565,7 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   wfpt::launch_multi(c->x.p, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
                      c->status, c->stream);
   HIP_TRY(hipGetLastError());
-  wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, c->mres_dev, c->stream);
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (int rc = check_status_value(c->mres[2])) return rc;

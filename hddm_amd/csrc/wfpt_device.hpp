@@ -742,7 +742,12 @@ __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, d
 //   * large-t series: the Chebyshev recurrence in k from the rotated sin/cos;
 //   * the drift factor exp(c_j): three exponentials and the second-difference
 //     recurrence (direct exps when |c| > 600).
-__device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
+#ifdef WFPT_EXP_NOINLINE
+__device__ __attribute__((noinline))
+#else
+__device__ inline
+#endif
+void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
                                           double a, double (&out)[5]) {
   double p[5];
 #pragma unroll
@@ -922,7 +927,9 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
     double y;
     if (MODE == kAdaptTZ) {
       y = level0_z(T, G, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
+#ifndef WFPT_EXP_NOEXIT
       if (slow) return 0.0;
+#endif
     } else {
       y = tnode_pdf_sv(T, z, v, sv, a) * iZt;
     }

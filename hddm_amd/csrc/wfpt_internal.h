@@ -20,9 +20,11 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
                    double* out, int* zeros, unsigned long long* evals, int* status, int logp,
                    unsigned char* wl, int* wl_n, hipStream_t s);
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
-// out[0..2] = {sum, #zero trials, status flags}; resets *status to 0.
+void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt);
+// out[0..2] = {sum, #zero trials, status flags}, then out[3] = seq (as a
+// 64-bit word) once they are visible; resets *status to 0.
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
-                     hipStream_t s);
+                     unsigned long long seq, hipStream_t s);
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, double* lp, unsigned long long* evals, int* status,
                   hipStream_t s);

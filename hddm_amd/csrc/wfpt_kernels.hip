@@ -251,15 +251,18 @@ __global__ WFPT_FAST_T_BOUNDS void fast_t_kernel(TrialArgs A, unsigned char* wl,
 }
 
 // General pass over the trials the fast pass deferred. The fast pass leaves
-// one worklist per 64 trials (nl lists); this one-wave-per-block kernel runs
-// on a bounded grid (kSlowGrid blocks) and block g walks lists g, g + G, ...,
+// one worklist and one partial per 64 trials (nl lists); this
+// one-wave-per-block kernel runs on a bounded grid of kSlowGrid blocks — one
+// wave per SIMD, which is all its register footprint (the general recursion,
+// ~255 VGPRs) lets reside anyway — and block g walks lists g, g + G, ...,
 // running the wl_n[b] deferred trials of list b on its first lanes (full
 // adaptive quadrature, reference recursion order). An empty list costs one
-// scalar load, so a workload with (almost) nothing deferred pays a short
-// launch, not one block per 64 trials. OUT_SUM partials go to
-// A.out[nb + g] / A.zeros[nb + g]: each lane sums its own trials in list
-// order, then the wave tree, so the total is deterministic for a given n.
-constexpr int64_t kSlowGrid = 4096;
+// scalar load, so a workload with (almost) nothing deferred pays one short
+// launch. For OUT_SUM the block also folds the fast partials of its lists
+// into its own (lane j takes list g + jG of each 64-list chunk) and writes
+// A.out[nb + g] / A.zeros[nb + g]: finalize then sums G values. Fixed order
+// for a given n.
+constexpr int64_t kSlowGrid = 1024;
 
 template <int MODE, int STK, bool COUNT, int OUT>
 __global__ __launch_bounds__(64) void slow_kernel(TrialArgs A, const unsigned char* wl,
@@ -269,22 +272,41 @@ __global__ __launch_bounds__(64) void slow_kernel(TrialArgs A, const unsigned ch
   double lp = 0.0;
   long long zc = 0;
   int ovf = 0;
-  for (int64_t b = blockIdx.x; b < nl; b += gridDim.x) {
-    const int cnt = wl_n[b];
-    if ((int)threadIdx.x >= cnt) continue;
-    const int64_t i = b * 64 + wl[b * 64 + threadIdx.x];
-    double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
-    if (OUT == OUT_ARRAY) {
-      p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);
-      A.out[i] = A.logp ? log(p) : p;
-    } else {
-      p = p * (1 - A.P.p_outlier) + A.wp_outlier;
-      const bool z = p == 0;
-      double l = 0.0;
-      if (z) zc += 1;
-      else l = log(p);
-      lp += l;
-      if (OUT == OUT_LOGP) A.out[i] = z ? -INFINITY : l;
+  const int lane = threadIdx.x;
+  const int64_t G = gridDim.x;
+  // chunks of 64 lists (g + j G, j = 0..63): one parallel load of their
+  // counts and fast partials, then only the non-empty lists are walked
+  for (int64_t b0 = blockIdx.x; b0 < nl; b0 += 64 * G) {
+    const int64_t myb = b0 + lane * G;
+    int mycnt = 0;
+    if (myb < nl) {
+      mycnt = wl_n[myb];
+      if (OUT == OUT_SUM) {
+        lp += A.out[myb];
+        zc += A.zeros[myb];
+      }
+    }
+    unsigned long long work = __ballot(mycnt > 0);
+    while (work) {
+      const int j = __ffsll((long long)work) - 1;
+      work &= work - 1;
+      const int cnt = __shfl(mycnt, j, 64);
+      const int64_t b = b0 + (int64_t)j * G;
+      if (lane >= cnt) continue;
+      const int64_t i = b * 64 + wl[b * 64 + lane];
+      double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
+      if (OUT == OUT_ARRAY) {
+        p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);
+        A.out[i] = A.logp ? log(p) : p;
+      } else {
+        p = p * (1 - A.P.p_outlier) + A.wp_outlier;
+        const bool z = p == 0;
+        double l = 0.0;
+        if (z) zc += 1;
+        else l = log(p);
+        lp += l;
+        if (OUT == OUT_LOGP) A.out[i] = z ? -INFINITY : l;
+      }
     }
   }
   if (ovf) atomicOr(A.status, ovf);
@@ -311,7 +333,8 @@ __host__ __device__ inline int64_t slow_grid(int64_t nl) { return nl < kSlowGrid
 // order for a given nb (4 independent accumulators per thread keep 4 loads
 // in flight).
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
-                                                        int64_t nb, int* status, double* out) {
+                                                        int64_t nb, int* status, double* out,
+                                                        unsigned long long seq) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -349,6 +372,10 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     out[0] = t;
     out[1] = (double)zz;
     out[2] = (double)st;
+    __threadfence_system();
+    // completion word, written after the results are visible: the host may
+    // poll it instead of waiting on the stream
+    reinterpret_cast<volatile unsigned long long*>(out)[3] = seq;
     __threadfence_system();
   }
 }
@@ -513,7 +540,22 @@ static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, in
   else launch_out<COUNT, OUT_LOGP>(mode, stk, A, nb, wl, wl_n, s);
 }
 
-// number of block partials launch_trials(OUT_SUM) leaves for finalize
+// Where launch_trials(OUT_SUM) leaves the partials finalize must sum: the
+// slow pass's G partials (which already fold the fast ones) for adaptive
+// modes, else every fast / trial-kernel partial.
+void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt) {
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  const int64_t nw = (n + 63) / 64;
+  if (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) {
+    *off = nw;
+    *cnt = slow_grid(nw);
+  } else {
+    *off = 0;
+    *cnt = (mode == kDirect) ? nw : blocks_for(n);
+  }
+}
+
+// size of the partial buffers launch_trials(OUT_SUM) writes
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   const int64_t nw = (n + 63) / 64;  // fast (and slow) partials are per 64 trials
@@ -551,8 +593,9 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
-                     hipStream_t s) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, status, out);
+                     unsigned long long seq, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, status, out,
+                     seq);
 }
 
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
