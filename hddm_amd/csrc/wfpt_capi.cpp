@@ -66,6 +66,31 @@ struct DevBuf {
   }
 };
 
+// Pinned host memory mapped into the device address space (fine-grained,
+// coherent): the host writes per-call inputs / reads results there directly.
+template <class T>
+struct MappedBuf {
+  T* h = nullptr;  // host pointer
+  T* d = nullptr;  // device alias
+  size_t cap = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= cap) return hipSuccess;
+    release();
+    const size_t want = std::max<size_t>(n, 64);
+    hipError_t e = hipHostMalloc((void**)&h, want * sizeof(T),
+                                 hipHostMallocMapped | hipHostMallocCoherent);
+    if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&d, h, 0);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (h) (void)hipHostFree(h);
+    h = nullptr;
+    d = nullptr;
+    cap = 0;
+  }
+};
+
 struct wfpt_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -89,6 +114,9 @@ struct wfpt_ctx {
   double* mres = nullptr;      // mapped pinned {sum, zeros, status}: finalize writes it
   double* mres_dev = nullptr;  // its device alias
   unsigned long long seq = 0;  // completion word finalize writes to mres[3]
+  MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
+  MappedBuf<double> mnode;         // per-node sums + status + completion word
+  unsigned* ticket = nullptr;      // device: last-block counter of segment_sum_kernel
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
@@ -236,17 +264,18 @@ int finish_profile(wfpt_ctx* c) {
   return WFPT_OK;
 }
 
-// Waits for the result of the last run_sum. For the mapped slot the host polls
-// the completion word finalize writes after the results (a stream sync's
-// wake-up costs several microseconds per call); every 4096 polls it asks the
-// stream whether it failed, and after 5 s it falls back to a stream sync so a
-// device error is reported, never a stale number.
-int wait_result(wfpt_ctx* c, const double* r) {
-  if (r == c->mres && c->spin) {
-    const volatile unsigned long long* w = reinterpret_cast<const volatile unsigned long long*>(r);
+// Waits for the completion word `word` (mapped host memory) to reach c->seq:
+// the last kernel of a call writes it after its results (a stream sync's
+// wake-up costs several microseconds per call). Every 4096 polls the stream is
+// asked whether it failed; after 5 s, or if the stream is idle without the
+// word, it falls back to a stream sync so a device error is reported, never a
+// stale number.
+int wait_word(wfpt_ctx* c, const void* word) {
+  if (c->spin) {
+    const volatile unsigned long long* w = reinterpret_cast<const volatile unsigned long long*>(word);
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
-      if (w[3] == c->seq) {
+      if (w[0] == c->seq) {
         std::atomic_thread_fence(std::memory_order_acquire);
         if (c->profile) HIP_TRY(hipEventSynchronize(c->ev1));
         return WFPT_OK;
@@ -255,11 +284,19 @@ int wait_result(wfpt_ctx* c, const double* r) {
         const hipError_t q = hipStreamQuery(c->stream);
         if (q != hipSuccess && q != hipErrorNotReady)
           return fail(WFPT_ERR_HIP, std::string("likelihood kernels: ") + hipGetErrorString(q));
-        if (q == hipSuccess && w[3] != c->seq) break;  // idle: let the stream sync decide
+        if (q == hipSuccess && w[0] != c->seq) break;  // idle: let the stream sync decide
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
       }
     }
   }
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (*reinterpret_cast<const volatile unsigned long long*>(word) != c->seq)
+    return fail(WFPT_ERR_HIP, "the call's completion word was not written");
+  return WFPT_OK;
+}
+
+int wait_result(wfpt_ctx* c, const double* r) {
+  if (r == c->mres) return wait_word(c, r + 3);
   HIP_TRY(hipStreamSynchronize(c->stream));
   return WFPT_OK;
 }
@@ -315,6 +352,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
     e = hipHostMalloc((void**)&c->mres, 4 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->ticket, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(unsigned));
   if (e != hipSuccess) {
     wfpt_close(c);
     return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
@@ -344,6 +383,9 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->host_status) (void)hipHostFree(c->host_status);
   if (c->host) (void)hipHostFree(c->host);
   if (c->mres) (void)hipHostFree(c->mres);
+  c->mnodep.release();
+  c->mnode.release();
+  if (c->ticket) (void)hipFree(c->ticket);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -502,30 +544,31 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
-  std::vector<wfpt::Params> hp(m);
-  for (int32_t j = 0; j < m; ++j) hp[j] = to_params(&per_node[j]);
-  HIP_TRY(c->nodep.reserve(m));
-  HIP_TRY(hipMemcpyAsync(c->nodep.p, hp.data(), m * sizeof(wfpt::Params), hipMemcpyHostToDevice,
-                         c->stream));
+  // the parameter table goes straight into mapped pinned memory: node_kernel
+  // stages the rows each block needs in LDS (no H2D copy per call)
+  HIP_TRY(c->mnodep.reserve(m));
+  for (int32_t j = 0; j < m; ++j) c->mnodep.h[j] = to_params(&per_node[j]);
+  HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
-  HIP_TRY(c->res.reserve(m));
-  if (int rc = begin_status(c)) return rc;
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  wfpt::launch_nodes(d->x, d->node, d->n, c->nodep.p, K, c->lp.p,
+  wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, c->lp.p,
                      c->count ? c->evals : nullptr, c->status, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->stream);
-  HIP_TRY(hipGetLastError());
-  if (int rc = ensure_host(c, m)) return rc;
-  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, m * sizeof(double), hipMemcpyDeviceToHost,
-                         c->stream));
-  if (int rc = fetch_status(c)) return rc;
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  if (int rc = check_status(c)) return rc;
+  ++c->seq;
+  if (m > 0) {
+    // per-node sums, status and the completion word land in mapped memory
+    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->mnode.d, c->status, c->ticket, c->seq,
+                             c->stream);
+    HIP_TRY(hipGetLastError());
+    if (int rc = wait_word(c, c->mnode.h + m + 1)) return rc;
+    if (int rc = check_status_value(c->mnode.h[m])) return rc;
+  } else {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
   if (int rc = finish_profile(c)) return rc;
-  std::memcpy(out, c->host, m * sizeof(double));
+  std::memcpy(out, c->mnode.h, m * sizeof(double));
   return WFPT_OK;
 }
 
@@ -567,7 +610,7 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   HIP_TRY(hipGetLastError());
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (int rc = wait_result(c, c->mres)) return rc;
   if (int rc = check_status_value(c->mres[2])) return rc;
   *out = c->mres[0];
   return WFPT_OK;

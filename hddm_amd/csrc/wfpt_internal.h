@@ -28,8 +28,10 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int* stat
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, double* lp, unsigned long long* evals, int* status,
                   hipStream_t s);
+// out (mapped host): [0, n_nodes) per-node sums, [n_nodes] status flags,
+// [n_nodes + 1] the 64-bit completion word seq (ticket: device counter, 0 at rest).
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
-                        hipStream_t s);
+                        int* status, unsigned* ticket, unsigned long long seq, hipStream_t s);
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
                   const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
                   hipStream_t s);

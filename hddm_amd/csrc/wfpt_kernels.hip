@@ -382,37 +382,81 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
 
 // One wave per node: sums per-trial log p of [off[j], off[j+1]) in fixed order.
 // out[j] = -inf if the node holds a zero-density trial (wfpt.pyx:71-72).
+// `out` is mapped pinned host memory: out[n_nodes] receives the call's status
+// flags and, once every block's results are visible, the 64-bit completion
+// word `seq` goes to out[n_nodes + 1] (written by the last block to finish,
+// found with a device-scope ticket counter that it resets for the next call).
 __global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, const int64_t* off,
-                                                          int32_t n_nodes, double* out) {
+                                                          int32_t n_nodes, double* out,
+                                                          int* status, unsigned* ticket,
+                                                          unsigned long long seq) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (j >= n_nodes) return;
-  const int64_t lo = off[j], hi = off[j + 1];
-  double s = 0.0;
-  int zero = 0;
-  for (int64_t i = lo + lane; i < hi; i += 64) {
-    const double v = lp[i];
-    if (v == -INFINITY) zero = 1;
-    else s += v;
+  if (j < n_nodes) {
+    const int64_t lo = off[j], hi = off[j + 1];
+    double s = 0.0;
+    int zero = 0;
+    for (int64_t i = lo + lane; i < hi; i += 64) {
+      const double v = lp[i];
+      if (v == -INFINITY) zero = 1;
+      else s += v;
+    }
+    s = wave_sum(s);
+    const bool anyz = __ballot(zero != 0) != 0ull;
+    if (lane == 0) {
+      out[j] = anyz ? -INFINITY : s;
+      __threadfence_system();
+    }
   }
-  s = wave_sum(s);
-  const bool anyz = __ballot(zero != 0) != 0ull;
-  if (lane == 0) out[j] = anyz ? -INFINITY : s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    const unsigned t = atomicAdd(ticket, 1u);
+    if (t == gridDim.x - 1) {
+      __threadfence();
+      const int st = atomicExch(status, 0);
+      *ticket = 0u;
+      out[n_nodes] = (double)st;
+      __threadfence_system();
+      reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
+      __threadfence_system();
+    }
+  }
 }
 
-// Per-node parameters: trials of node j read P[j] (wfpt_wiener_like_nodes).
+// Per-node parameters (wfpt_wiener_like_nodes): trials of node j use P[j].
+// The dataset is grouped by node, so a 256-trial block spans a short run of
+// node ids; their parameter rows (P is the mapped pinned table the host
+// filled for this call) are staged once per block in LDS and every trial
+// reads its row there. Blocks spanning more than kStageRows ids (empty nodes
+// between) read the table directly.
+constexpr int kStageRows = 256;
+
 template <int STK, bool COUNT>
 __global__ __launch_bounds__(kBlock) void node_kernel(const double* x, const int32_t* node,
                                                       int64_t n, const Params* P, Knobs K,
                                                       double* lp, unsigned long long* evals,
                                                       int* status) {
   using Stack = typename StackOf<STK>::type;
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  __shared__ Params rows[kStageRows];
+  const int64_t i0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t i = i0 + threadIdx.x;
+  const int first = node[i0];
+  const int last = node[(i0 + kBlock - 1 < n) ? i0 + kBlock - 1 : n - 1];
+  const int span = last - first + 1;
+  const bool staged = span <= kStageRows;
+  if (staged) {
+    const double* src = reinterpret_cast<const double*>(P + first);
+    double* dst = reinterpret_cast<double*>(rows);
+    for (int k = threadIdx.x; k < span * 8; k += kBlock) dst[k] = src[k];
+  }
+  __syncthreads();
   long long ne = 0;
   double out = 0.0;
   int zero = 0, ovf = 0;
   if (i < n) {
-    const Params Q = P[node[i]];
+    const int nj = node[i];
+    const Params Q = staged ? rows[nj - first] : P[nj];
     double p = full_pdf<kRuntime, Stack, COUNT>(x[i], Q, K, ne, ovf);
     if (ovf) atomicOr(status, ovf);
     const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);
@@ -620,10 +664,10 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
 }
 
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
-                        hipStream_t s) {
+                        int* status, unsigned* ticket, unsigned long long seq, hipStream_t s) {
   if (n_nodes <= 0) return;
   hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                     n_nodes, out);
+                     n_nodes, out, status, ticket, seq);
 }
 
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
