@@ -133,7 +133,10 @@ struct TNode {
   int pos;      // xx > 0 (else density 0, pdf.pxi:92)
 };
 
-__device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err) {
+// qhint >= 0: exp(-pi^2 tt / 2) of this node computed by the caller (a
+// recurrence over the t grid); < 0: computed here.
+__device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err,
+                                    double qhint = -1.0) {
   TNode T;
   T.xx = xx;
   T.pos = xx > 0;
@@ -211,19 +214,33 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   if (ks < kl) {
     T.small = 1;
     T.K = (int)ceil(ks);
-    T.rn = 1.0 / sqrt((2.0 * kPi) * ((tt * tt) * tt));  // value only: pow(tt,3) to 1 ulp
+#if WFPT_EXACT_MATH
+    T.rn = 1.0 / sqrt((2.0 * kPi) * ((tt * tt) * tt));
+#else
+    T.rn = rsqrt((2.0 * kPi) * ((tt * tt) * tt));  // value only: 1/sqrt(2 pi tt^3)
+#endif
     T.m = -0.5 / tt;
   } else {
     T.small = 0;
     T.K = (int)ceil(kl);
-    T.m = exp((-kPi2 * tt) / 2.0);
+    T.m = qhint >= 0.0 ? qhint : exp((-kPi2 * tt) / 2.0);
     T.q2 = T.m * T.m;
   }
+#if WFPT_EXACT_MATH
   T.sc = 1.0 / a2;
   if (sv != 0) {
     T.cden = 1.0 / (((2.0 * (sv * sv)) * xx) + 2.0);
     T.sc = T.sc / sqrt(((sv * sv) * xx) + 1.0);
   }
+#else
+  // values only: 1/(2u) and 1/(a^2 sqrt(u)), u = sv^2 xx + 1, from one rsqrt
+  T.sc = 1.0 / a2;
+  if (sv != 0) {
+    const double r = rsqrt(((sv * sv) * xx) + 1.0);
+    T.cden = (0.5 * r) * r;
+    T.sc = T.sc * r;
+  }
+#endif
   T.vvx = (v * v) * xx;
   return T;
 }
@@ -811,18 +828,29 @@ void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
       skm1[i] = 0.0;
       if (K >= 1) p[i] = T.m * sj[i];
     }
+    // two terms per trip, the two sin registers swapping roles (no moves)
     double e = T.m, r = T.m * T.q2;
-    for (int k = 2; k <= K; ++k) {
+    int k = 2;
+    for (; k + 1 <= K; k += 2) {
       e = e * r;
       r = r * T.q2;
       const double ke = (double)k * e;
+      e = e * r;
+      r = r * T.q2;
+      const double ke1 = (double)(k + 1) * e;
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const double sn = tc[i] * sk[i] - skm1[i];
-        skm1[i] = sk[i];
-        sk[i] = sn;
-        p[i] = p[i] + ke * sk[i];
+        skm1[i] = tc[i] * sk[i] - skm1[i];  // sin(k pi w)
+        p[i] = p[i] + ke * skm1[i];
+        sk[i] = tc[i] * skm1[i] - sk[i];    // sin((k+1) pi w)
+        p[i] = p[i] + ke1 * sk[i];
       }
+    }
+    if (k <= K) {
+      e = e * r;
+      const double ke = (double)k * e;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) p[i] = p[i] + ke * (tc[i] * sk[i] - skm1[i]);
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = p[i] * kPi;
@@ -919,11 +947,29 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
   const double iZt = 1.0 / (ub - lb);
   ZGrid G;
   if (MODE == kAdaptTZ) G = zgrid_setup(lbz, ubz, v, sv, a);
+  // large-time factor q = exp(-pi^2 (x - tc) / (2 a^2)) over the t grid:
+  // q(lb + k (ub - lb) / 4) = q(lb) R^k with R = exp(pi^2 (ub - lb) / (8 a^2))
+  // (values only; direct exps where the products leave the safe range)
+  double qn[5] = {-1.0, -1.0, -1.0, -1.0, -1.0};
+  {
+    const double a2 = a * a;
+    const double q0 = exp((-kPi2 * ((x - lb) / a2)) / 2.0);
+    const double R = exp((kPi2 * (ub - lb)) / (8.0 * a2));
+    if (!WFPT_EXACT_MATH && q0 > 1e-280 && R < 1e10 && x - lb > 0) {
+      const double R2 = R * R;
+      qn[0] = q0;           // lb
+      qn[1] = q0 * (R2 * R2);  // ub
+      qn[2] = q0 * R2;      // c
+      qn[3] = q0 * R;       // d
+      qn[4] = q0 * (R2 * R);   // e
+    }
+  }
   double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
 #pragma unroll 1
   for (int j = 0; j < 5; ++j) {
     const double tc = j == 0 ? lb : j == 1 ? ub : j == 2 ? c : j == 3 ? d : e;
-    const TNode T = tnode_setup(x - tc, v, sv, a, err);
+    const double qh = j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
+    const TNode T = tnode_setup(x - tc, v, sv, a, err, qh);
     double y;
     if (MODE == kAdaptTZ) {
       y = level0_z(T, G, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
