@@ -6,11 +6,16 @@
 //                    drift x 6-point Gauss-Legendre over the start point, series in
 //                    the boundary eigenfunctions, closed-form integral over Ter)
 //
-// Layout: one trial per lane (wave64, 256-thread blocks). Everything that
-// depends only on the call's parameters — the scaled quadrature nodes and
-// weights, log(w_gh), and P(boundary) (cdfdif.c:84-113: 36 exp pairs) — is
-// computed once per block by its first wave into LDS and read by every lane
-// as broadcast loads; the per-trial series run in registers.
+// Layout: everything that depends only on the call's parameters — the scaled
+// quadrature nodes and weights, log(w_gh), and P(boundary) (cdfdif.c:84-113:
+// 36 exp pairs) — is computed once per block by its first wave into LDS and
+// read by every lane as broadcast loads. Two passes:
+//   dmat_cdf_kernel  one trial per lane (wave64, 256-thread blocks); finishes
+//                    trials below the Ter window and beyond it when the series
+//                    converges within kLaneTerms terms, defers the rest;
+//   cdf_wave_kernel  one wave per deferred trial: the terms of 64 consecutive
+//                    v in parallel (sequential accumulation in v order), or
+//                    the 36 + 6 window-branch series one per lane.
 //
 // Numerics: every basic operation follows the reference's expression order
 // (-ffp-contract=off), and the transcendental calls are the reference's
@@ -103,116 +108,234 @@ __device__ inline bool converged(double h0, double h1, double h2) {
   return (fabs(h0 - h1) < kDelta) && (fabs(h1 - h2) < kDelta) && (h2 > 0);
 }
 
-// cdfdif(t, x, par, &prob) for one trial (cdfdif.c:59-221); prob is S.prob.
-__device__ inline double cdf_trial(double t, int x, const CdfPar& P, const CdfShared& S) {
+// Per-trial quantities of cdfdif (cdfdif.c:61-69, 116-120) and its branch:
+// 0 = t below the Ter window (F = 0, :213-216), 1 = beyond it (:121-149),
+// 2 = inside it (:151-211).
+struct CdfTrial {
+  double t, Z_U, Z_L, lower_t, upper_t, p0, p1;
+  int x, sg, sh, branch;
+};
+
+__device__ inline CdfTrial cdf_prepare(double t, int x, const CdfPar& P, const CdfShared& S) {
   const double a = P.a, Ter = P.Ter, sZ = P.sZ, st = P.st, z = P.z;
-  const double a2 = a * a;
-  const double Z_U = (((1 - x) * z) + (x * (a - z))) + (sZ / 2);
-  const double Z_L = (((1 - x) * z) + (x * (a - z))) - (sZ / 2);
-  const double lower_t = Ter - (st / 2);
-  const int sg = 2 * x - 1;  // (2*x-1)
-  const int sh = 1 - 2 * x;  // (1-2*x)
-  const double l100 = log(100.);
-  double Fnew = 0.0;
+  CdfTrial T;
+  T.t = t;
+  T.x = x;
+  T.Z_U = (((1 - x) * z) + (x * (a - z))) + (sZ / 2);
+  T.Z_L = (((1 - x) * z) + (x * (a - z))) - (sZ / 2);
+  T.lower_t = Ter - (st / 2);
+  T.sg = 2 * x - 1;  // (2*x-1)
+  T.sh = 1 - 2 * x;  // (1-2*x)
+  T.branch = 0;
+  T.upper_t = T.p0 = T.p1 = 0.0;
   if (((t - Ter) + (st / 2)) > kMinRT) {
-    const double upper_t = t < (Ter + (st / 2)) ? t : (Ter + (st / 2));
-    const double p1 = (S.prob * (upper_t - lower_t)) / st;
-    const double p0 = ((1 - S.prob) * (upper_t - lower_t)) / st;
-    if (t > (Ter + (st / 2))) {  // cdfdif.c:121-149
-      double h0 = 0, h1 = 0, h2 = 0;
-      for (int v = 0; v < kVMax; ++v) {
-        h0 = h1;
-        h1 = h2;
-        double sum_nu = 0;
-        const double sifa = (kCPi * v) / a;
-        const double sU = sin(sifa * Z_U), cU = cos(sifa * Z_U);
-        const double sL = sin(sifa * Z_L), cL = cos(sifa * Z_L);
-        const double pv = ((kCPi * kCPi) * (double)(v * v)) / (100 * a2);
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          const double g = S.gk[m];
-          const double denom = ((100 * g) * g) + pv;
-          const double ld = 3 * log(denom);
-          const double upp = exp(((((sg * Z_U) * g) * 100) - ld + S.lw[m]) - (2 * l100));
-          const double low = exp(((((sg * Z_L) * g) * 100) - ld + S.lw[m]) - (2 * l100));
-          const double fact = (upp * ((((sg * g) * sU) * 100) - (sifa * cU))) -
-                              (low * ((((sg * g) * sL) * 100) - (sifa * cL)));
-          const double exdif = exp(((-.5 * denom) * (t - upper_t)) +
-                                   log(1 - exp((-.5 * denom) * (upper_t - lower_t))));
-          sum_nu += fact * exdif;
-        }
-        h2 = h1 + v * sum_nu;
-        if (converged(h0, h1, h2)) break;
-      }
-      Fnew = ((p0 * (1 - x)) + (p1 * x)) - (((h2 * 4) * kCPi) / ((a2 * sZ) * st));
-    } else {  // t inside the Ter window, cdfdif.c:151-211
-      double sum_nu = 0;
-      for (int m = 0; m < 6; ++m) {
-        const double g = S.gk[m];
-        double sum_z = 0;
-        if (fabs(g) > kEps) {
-          const double B = ((sh * g) * kCPi) * .01;
-          const double D = ((sh * g) * a) / .01;
-          const double sD = sinh(D);
-          for (int i = 0; i < 6; ++i) {
-            const double gzi = S.gz[i];
-            const double zzz = ((a - gzi) * x) + (gzi * (1 - x));
-            const double ser = (((-((a * a2) / B)) * sinh(((zzz * sh) * g) / .01)) / (sD * sD)) +
-                               ((((zzz * a2) / B) * cosh((((a - zzz) * sh) * g) / .01)) / sD);
-            double h0 = 0, h1 = 0, h2 = 0;
-            for (int v = 0; v < kVMax; ++v) {
-              h0 = h1;
-              h1 = h2;
-              const double sifa = (kCPi * v) / a;
-              const double denom =
-                  ((g * g) * 100) + (((kCPi * v) * (kCPi * v)) / (a2 * 100));
-              h2 = h1 + ((v * sin(sifa * zzz)) *
-                         exp(((-.5 * denom) * (t - lower_t)) - (2 * log(denom))));
-              if (converged(h0, h1, h2)) break;
-            }
-            sum_z += ((((.5 * S.w_g[i]) * (ser - (4 * h2))) * (kCPi / 100)) / (a2 * st)) *
-                     exp((((sg * zzz) * g) * 100));
-          }
-        } else {
-          const double su = ((-(Z_U * Z_U)) / (12 * a2) + ((Z_U * Z_U) * Z_U) / ((12 * a) * a2)) -
-                            ((((Z_U * Z_U) * Z_U) * Z_U) / ((48 * a2) * a2));
-          const double sl = ((-(Z_L * Z_L)) / (12 * a2) + ((Z_L * Z_L) * Z_L) / ((12 * a) * a2)) -
-                            ((((Z_L * Z_L) * Z_L) * Z_L) / ((48 * a2) * a2));
-          double h0 = 0, h1 = 0, h2 = 0;
-          for (int v = 1; v < kVMax; ++v) {
-            h0 = h1;
-            h1 = h2;
-            const double sifa = (kCPi * v) / a;
-            const double denom = ((kCPi * v) * (kCPi * v)) / (a2 * 100);
-            h2 = h1 + (((1 / ((((((((kCPi * kCPi) * kCPi) * kCPi) * v) * v) * v) * v))) *
-                        (cos(sifa * Z_L) - cos(sifa * Z_U))) *
-                       exp((-.5 * denom) * (t - lower_t)));
-            if (converged(h0, h1, h2)) break;
-          }
-          sum_z = (((400 * a2) * a) * ((sl - su) - h2)) / (st * sZ);
-        }
-        sum_nu += sum_z * S.w_gh[m];
-      }
-      Fnew = ((p0 * (1 - x)) + (p1 * x)) - sum_nu;
-    }
+    T.upper_t = t < (Ter + (st / 2)) ? t : (Ter + (st / 2));
+    T.p1 = (S.prob * (T.upper_t - T.lower_t)) / st;
+    T.p0 = ((1 - S.prob) * (T.upper_t - T.lower_t)) / st;
+    T.branch = (t > (Ter + (st / 2))) ? 1 : 2;
   }
-  return Fnew > kDelta ? Fnew : 0;  // cdfdif.c:218 (NaN -> 0 as well)
+  return T;
 }
+
+// Term v of the series beyond the window, v * sum_nu (cdfdif.c:130-143).
+__device__ inline double beyond_term(int v, const CdfTrial& T, const CdfPar& P,
+                                     const CdfShared& S) {
+  const double a = P.a, a2 = a * a, t = T.t, upper_t = T.upper_t, lower_t = T.lower_t;
+  const double Z_U = T.Z_U, Z_L = T.Z_L;
+  const int sg = T.sg;
+  const double l100 = log(100.);
+  double sum_nu = 0;
+  const double sifa = (kCPi * v) / a;
+  const double sU = sin(sifa * Z_U), cU = cos(sifa * Z_U);
+  const double sL = sin(sifa * Z_L), cL = cos(sifa * Z_L);
+  const double pv = ((kCPi * kCPi) * (double)(v * v)) / (100 * a2);
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const double g = S.gk[m];
+    const double denom = ((100 * g) * g) + pv;
+    const double ld = 3 * log(denom);
+    const double upp = exp(((((sg * Z_U) * g) * 100) - ld + S.lw[m]) - (2 * l100));
+    const double low = exp(((((sg * Z_L) * g) * 100) - ld + S.lw[m]) - (2 * l100));
+    const double fact = (upp * ((((sg * g) * sU) * 100) - (sifa * cU))) -
+                        (low * ((((sg * g) * sL) * 100) - (sifa * cL)));
+    const double exdif = exp(((-.5 * denom) * (t - upper_t)) +
+                             log(1 - exp((-.5 * denom) * (upper_t - lower_t))));
+    sum_nu += fact * exdif;
+  }
+  return v * sum_nu;
+}
+
+__device__ inline double beyond_F(double h2, const CdfTrial& T, const CdfPar& P) {
+  const double a2 = P.a * P.a;
+  return ((T.p0 * (1 - T.x)) + (T.p1 * T.x)) - (((h2 * 4) * kCPi) / ((a2 * P.sZ) * P.st));  // :148
+}
+
+// Window branch, drift node m with |gk| > eps, start-point node i: the
+// increment of sum_z (cdfdif.c:161-182).
+__device__ inline double window_mi(int m, int i, const CdfTrial& T, const CdfPar& P,
+                                   const CdfShared& S) {
+  const double a = P.a, a2 = a * a, st = P.st, t = T.t, lower_t = T.lower_t;
+  const int x = T.x, sg = T.sg, sh = T.sh;
+  const double g = S.gk[m];
+  const double B = ((sh * g) * kCPi) * .01;
+  const double sD = sinh(((sh * g) * a) / .01);
+  const double gzi = S.gz[i];
+  const double zzz = ((a - gzi) * x) + (gzi * (1 - x));
+  const double ser = (((-((a * a2) / B)) * sinh(((zzz * sh) * g) / .01)) / (sD * sD)) +
+                     ((((zzz * a2) / B) * cosh((((a - zzz) * sh) * g) / .01)) / sD);
+  double h0 = 0, h1 = 0, h2 = 0;
+  for (int v = 0; v < kVMax; ++v) {
+    h0 = h1;
+    h1 = h2;
+    const double sifa = (kCPi * v) / a;
+    const double denom = ((g * g) * 100) + (((kCPi * v) * (kCPi * v)) / (a2 * 100));
+    h2 = h1 + ((v * sin(sifa * zzz)) * exp(((-.5 * denom) * (t - lower_t)) - (2 * log(denom))));
+    if (converged(h0, h1, h2)) break;
+  }
+  return ((((.5 * S.w_g[i]) * (ser - (4 * h2))) * (kCPi / 100)) / (a2 * st)) *
+         exp((((sg * zzz) * g) * 100));
+}
+
+// Window branch, drift node ~ 0: sum_z (cdfdif.c:187-206).
+__device__ inline double window_m0(const CdfTrial& T, const CdfPar& P) {
+  const double a = P.a, a2 = a * a, st = P.st, sZ = P.sZ, t = T.t, lower_t = T.lower_t;
+  const double Z_U = T.Z_U, Z_L = T.Z_L;
+  const double su = ((-(Z_U * Z_U)) / (12 * a2) + ((Z_U * Z_U) * Z_U) / ((12 * a) * a2)) -
+                    ((((Z_U * Z_U) * Z_U) * Z_U) / ((48 * a2) * a2));
+  const double sl = ((-(Z_L * Z_L)) / (12 * a2) + ((Z_L * Z_L) * Z_L) / ((12 * a) * a2)) -
+                    ((((Z_L * Z_L) * Z_L) * Z_L) / ((48 * a2) * a2));
+  double h0 = 0, h1 = 0, h2 = 0;
+  for (int v = 1; v < kVMax; ++v) {
+    h0 = h1;
+    h1 = h2;
+    const double sifa = (kCPi * v) / a;
+    const double denom = ((kCPi * v) * (kCPi * v)) / (a2 * 100);
+    h2 = h1 + (((1 / ((((((((kCPi * kCPi) * kCPi) * kCPi) * v) * v) * v) * v))) *
+                (cos(sifa * Z_L) - cos(sifa * Z_U))) *
+               exp((-.5 * denom) * (t - lower_t)));
+    if (converged(h0, h1, h2)) break;
+  }
+  return (((400 * a2) * a) * ((sl - su) - h2)) / (st * sZ);
+}
+
+// cdfdif.c:218 (a NaN ends as 0 too), then the wrapper's fold and outlier mix
+// (cdfdif_wrapper.pyx:48, 11-12, 51).
+__device__ inline double cdf_output(double Fnew, double xi, double p_outlier, double w_outlier,
+                                    const CdfShared& S) {
+  double y = Fnew > kDelta ? Fnew : 0;
+  const double sgn = xi > 0 ? 1.0 : (xi < 0 ? -1.0 : (xi == 0 ? 0.0 : xi));  // np.sign
+  y = (1 - S.prob) + (sgn * y);
+  return (y * (1 - p_outlier)) + (((xi + (1. / (2 * w_outlier))) * w_outlier) * p_outlier);
+}
+
+// Per-lane pass: trials below the window, and trials beyond it whose series
+// converges within kLaneTerms terms, are finished here. The rest — window
+// trials (36 series of up to 5000 terms each) and slowly converging series
+// near the window edge — are appended to `defer` (their cost would otherwise
+// hold a whole wave) for cdf_wave_kernel.
+constexpr int kLaneTerms = 48;
 
 __global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, int64_t n,
                                                              CdfPar P, double p_outlier,
-                                                             double w_outlier, double* out) {
+                                                             double w_outlier, double* out,
+                                                             int* defer, int* n_defer) {
   __shared__ CdfShared S;
   cdf_setup(P, S);
   const int64_t i = (int64_t)blockIdx.x * kCdfBlock + threadIdx.x;
-  if (i >= n) return;
-  const double xi = xs[i];
-  const int boundary = xi > 0;  // cdfdif_wrapper.pyx:46
-  double y = cdf_trial(fabs(xi), boundary, P, S);
-  const double sgn = xi > 0 ? 1.0 : (xi < 0 ? -1.0 : (xi == 0 ? 0.0 : xi));  // np.sign
-  y = (1 - S.prob) + (sgn * y);                                              // :48
-  y = (y * (1 - p_outlier)) + (((xi + (1. / (2 * w_outlier))) * w_outlier) * p_outlier);  // :11-12
-  out[i] = y;
+  bool deferred = false;
+  if (i < n) {
+    const double xi = xs[i];
+    const CdfTrial T = cdf_prepare(fabs(xi), xi > 0, P, S);  // boundary, cdfdif_wrapper.pyx:46
+    double F = 0.0;
+    if (T.branch == 1) {
+      double h0 = 0, h1 = 0, h2 = 0;
+      bool conv = false;
+      for (int v = 0; v < kLaneTerms; ++v) {
+        h0 = h1;
+        h1 = h2;
+        h2 = h1 + beyond_term(v, T, P, S);
+        if (converged(h0, h1, h2)) {
+          conv = true;
+          break;
+        }
+      }
+      if (conv) F = beyond_F(h2, T, P);
+      else deferred = true;
+    } else if (T.branch == 2) {
+      deferred = true;
+    }
+    if (!deferred) out[i] = cdf_output(F, xi, p_outlier, w_outlier, S);
+  }
+  // wave-aggregated append (order irrelevant: outputs are per trial)
+  const unsigned long long b = __ballot(deferred);
+  if (b) {
+    const int lane = threadIdx.x & 63;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
+    base = __shfl(base, 0, 64);
+    if (deferred) defer[base + __popcll(b & ((1ull << lane) - 1ull))] = (int)i;
+  }
+}
+
+// One wave per deferred trial. Beyond the window: the terms of 64
+// consecutive v are computed one per lane, then accumulated in v order with
+// the reference's convergence test (sequential sum, so the partial sums are
+// the reference's). Inside the window: lane m*6+i runs the (m, i) series,
+// lanes 36+m the drift-node-~0 series, and sum_z / sum_nu are combined in the
+// reference's order.
+__global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P,
+                                                     double p_outlier, double w_outlier,
+                                                     double* out, const int* defer,
+                                                     const int* n_defer) {
+  __shared__ CdfShared S;
+  cdf_setup(P, S);
+  const int lane = threadIdx.x;
+  const int nd = *n_defer;
+  for (int k = blockIdx.x; k < nd; k += gridDim.x) {
+    const int idx = defer[k];
+    const double xi = xs[idx];
+    const CdfTrial T = cdf_prepare(fabs(xi), xi > 0, P, S);
+    double F;
+    if (T.branch == 1) {
+      double h0 = 0, h1 = 0, h2 = 0;
+      bool conv = false;
+      for (int v0 = 0; v0 < kVMax && !conv; v0 += 64) {
+        const int v = v0 + lane;
+        const double term = v < kVMax ? beyond_term(v, T, P, S) : 0.0;
+        const int m = (kVMax - v0 < 64) ? kVMax - v0 : 64;
+        for (int j = 0; j < m; ++j) {
+          h0 = h1;
+          h1 = h2;
+          h2 = h1 + __shfl(term, j, 64);
+          if (converged(h0, h1, h2)) {
+            conv = true;
+            break;
+          }
+        }
+      }
+      F = beyond_F(h2, T, P);
+    } else {
+      double val = 0.0;
+      if (lane < 36) {
+        const int m = lane / 6, i = lane % 6;
+        if (fabs(S.gk[m]) > kEps) val = window_mi(m, i, T, P, S);
+      } else if (lane < 42) {
+        if (!(fabs(S.gk[lane - 36]) > kEps)) val = window_m0(T, P);
+      }
+      double sum_nu = 0;
+      for (int m = 0; m < 6; ++m) {
+        double sum_z = 0;
+        if (fabs(S.gk[m]) > kEps) {
+          for (int i = 0; i < 6; ++i) sum_z += __shfl(val, m * 6 + i, 64);
+        } else {
+          sum_z = __shfl(val, 36 + m, 64);
+        }
+        sum_nu += sum_z * S.w_gh[m];
+      }
+      F = ((T.p0 * (1 - T.x)) + (T.p1 * T.x)) - sum_nu;  // cdfdif.c:210
+    }
+    if (lane == 0) out[idx] = cdf_output(F, xi, p_outlier, w_outlier, S);
+  }
 }
 
 }  // namespace
@@ -221,7 +344,7 @@ __global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, i
 // wrapper's transformed parameters (a/10, t, sv/10+1e-10, z*a/10,
 // sz*a/10+1e-10, st+1e-10, v/10).
 void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
-                     double w_outlier, double* out, hipStream_t s) {
+                     double w_outlier, double* out, int* defer, int* n_defer, hipStream_t s) {
   if (n <= 0) return;
   CdfPar P;
   P.a = par[0];
@@ -232,8 +355,13 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   P.st = par[5];
   P.nu = par[6];
   const int64_t nb = (n + kCdfBlock - 1) / kCdfBlock;
+  (void)hipMemsetAsync(n_defer, 0, sizeof(int), s);
   hipLaunchKernelGGL(dmat_cdf_kernel, dim3(nb), dim3(kCdfBlock), 0, s, x, n, P, p_outlier,
-                     w_outlier, out);
+                     w_outlier, out, defer, n_defer);
+  // one wave per deferred trial on a fixed grid (it reads the count itself)
+  const int64_t gw = n < 4096 ? n : 4096;
+  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, p_outlier, w_outlier, out,
+                     defer, n_defer);
 }
 
 }  // namespace wfpt

@@ -106,6 +106,7 @@ struct wfpt_ctx {
   DevBuf<double> mscal;
   DevBuf<unsigned char> wl;  // fast-pass worklists (lane ids per block)
   DevBuf<int> wl_n;          // deferred trials per block
+  DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
@@ -378,6 +379,7 @@ void wfpt_close(wfpt_ctx* c) {
   c->mscal.release();
   c->wl.release();
   c->wl_n.release();
+  c->defer.release();
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -627,6 +629,7 @@ int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_para
       (z - sz / 2. < 0) || (t - st / 2. < 0) || (t < 0) || (st < 0) || !p_outlier_in_range(po))
     return fail(WFPT_ERR_ARG, "at least one of the parameters is out of the support");
   if (n == 0) return WFPT_OK;
+  if (n >= (int64_t)1 << 31) return fail(WFPT_ERR_ARG, "dmat_cdf_array: n must be < 2^31");
   // cdfdif_wrapper.pyx:35-42 (the model's units: a and z scaled by 1/10, s = 0.1)
   const double epsi = 1e-10;
   const double par[7] = {a / 10., t, sv / 10. + epsi, z * (a / 10.), sz * (a / 10.) + epsi,
@@ -636,7 +639,9 @@ int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_para
   if (int rc = upload(c, x, n)) return rc;
   HIP_TRY(c->lp.reserve(n));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  wfpt::launch_dmat_cdf(c->x.p, n, par, po, w_outlier, c->lp.p, c->stream);
+  HIP_TRY(c->defer.reserve(n + 1));
+  wfpt::launch_dmat_cdf(c->x.p, n, par, po, w_outlier, c->lp.p, c->defer.p, c->defer.p + n,
+                        c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   HIP_TRY(hipMemcpyAsync(out, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));

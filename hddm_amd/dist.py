@@ -2,8 +2,8 @@
 
 The likelihood shards trivially (trials are independent): each
 rank keeps a contiguous trial range resident and the only exchange is one
-2-double ncclAllReduce of {sum log p, #zero-density trials} per call, done
-inside libwfpt_amd (wfpt_wiener_like_allreduce). torch.distributed (gloo, on
+3-double ncclAllReduce of {sum log p, #zero-density trials, status} per call,
+done inside libwfpt_amd (wfpt_wiener_like_allreduce). torch.distributed (gloo, on
 the host) is used only to broadcast RCCL's 128-byte unique id and for
 barriers / max-over-ranks timing in bench.py.
 """

@@ -40,7 +40,7 @@ def _worker(rank, world, port, x, args, kn, out_q):
     zeros = int(np.isneginf(lp).sum())
     s = math.fsum(lp[np.isfinite(lp)]) if zeros == 0 else 0.0
     t = torch.tensor([s, float(zeros)], dtype=torch.float64)
-    dist.all_reduce(t)  # the same 2-double sum RCCL does in wfpt_wiener_like_allreduce
+    dist.all_reduce(t)  # the {sum, zeros} part of RCCL's 3-double sum in wfpt_wiener_like_allreduce
     total = -math.inf if t[1].item() > 0 else t[0].item()
     out_q.put((rank, total, hi - lo))
     dist.barrier()
@@ -72,3 +72,26 @@ def test_two_rank_allreduce_matches_unsharded(oracle_lib, inject_zero):
             assert total == -math.inf and ref == -math.inf
         else:
             assert abs(total - ref) < 1e-9 * abs(ref)
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_allreduce_path(gpu, oracle_lib):
+    """The RCCL path of wfpt_wiener_like_allreduce on one GPU (world 1): the
+    3-double all-reduce must leave the local result unchanged, including the
+    zero-trial (-inf) semantics."""
+    from hddm_amd import _lib, dist as hdist
+    ctx = _lib.context()
+    hdist.init_comm(ctx, 0, 1)
+    rng = np.random.default_rng(3)
+    x = rng.choice([-1.0, 1.0], 50_000) * (0.35 + rng.gamma(2.0, 0.4, 50_000))
+    args = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    ds = gpu.Dataset(x)
+    a = ds.wiener_like_allreduce(*args, *kn)
+    b = ds.wiener_like(*args, *kn)
+    assert a == b
+    ref = oracle_lib.pdf_array(x, *args, kn[0], 1, *kn[1:])
+    assert abs(a - math.fsum(ref)) < 1e-11 * math.fsum(np.abs(ref))
+    x[17] = 0.1
+    ds0 = gpu.Dataset(x)
+    assert ds0.wiener_like_allreduce(*args, 1e-4, 2, 2, 1, 1e-3, 0.0, 0.1) == -math.inf
