@@ -107,6 +107,9 @@ struct wfpt_ctx {
   DevBuf<unsigned char> wl;  // fast-pass worklists (lane ids per block)
   DevBuf<int> wl_n;          // deferred trials per block
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
+  DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
+  DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
+  int* n_defer = nullptr;    // device: deferred count of the per-node fast path (0 at rest)
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
@@ -119,6 +122,7 @@ struct wfpt_ctx {
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   unsigned* ticket = nullptr;      // device: last-block counter of segment_sum_kernel
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
+  bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
   double k_ms = 0.0;
@@ -342,6 +346,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   auto* c = new wfpt_ctx();
   c->device = device;
   if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
+  if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -355,6 +360,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->ticket, sizeof(unsigned));
   if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
   if (e != hipSuccess) {
     wfpt_close(c);
     return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
@@ -380,6 +387,9 @@ void wfpt_close(wfpt_ctx* c) {
   c->wl.release();
   c->wl_n.release();
   c->defer.release();
+  c->nd_idx.release();
+  c->nd_par.release();
+  if (c->n_defer) (void)hipFree(c->n_defer);
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -549,20 +559,32 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   // the parameter table goes straight into mapped pinned memory: node_kernel
   // stages the rows each block needs in LDS (no H2D copy per call)
   HIP_TRY(c->mnodep.reserve(m));
-  for (int32_t j = 0; j < m; ++j) c->mnodep.h[j] = to_params(&per_node[j]);
+  int mode = -2;  // the integration family every node selects, or -1 if mixed
+  for (int32_t j = 0; j < m; ++j) {
+    c->mnodep.h[j] = to_params(&per_node[j]);
+    const int mj = wfpt::select_mode(per_node[j].sz, per_node[j].st, K.use_adaptive);
+    mode = (mode == -2 || mode == mj) ? mj : -1;
+  }
+  if (mode > wfpt::kAdaptTZ) mode = -1;  // fixed Simpson: generic kernel
+  if (c->nodes_generic) mode = -1;
+  if (mode >= 0) {  // deferred-trial records of the per-node fast path
+    HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
+    HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
+  }
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, c->lp.p,
-                     c->count ? c->evals : nullptr, c->status, c->stream);
+  wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, mode, c->lp.p, c->nd_idx.p,
+                     c->nd_par.p, c->n_defer, c->count ? c->evals : nullptr, c->status,
+                     c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   ++c->seq;
   if (m > 0) {
     // per-node sums, status and the completion word land in mapped memory
-    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->mnode.d, c->status, c->ticket, c->seq,
-                             c->stream);
+    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->mnode.d, c->status, c->ticket, c->n_defer,
+                             c->seq, c->stream);
     HIP_TRY(hipGetLastError());
     if (int rc = wait_word(c, c->mnode.h + m + 1)) return rc;
     if (int rc = check_status_value(c->mnode.h[m])) return rc;

@@ -389,6 +389,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
 __global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, const int64_t* off,
                                                           int32_t n_nodes, double* out,
                                                           int* status, unsigned* ticket,
+                                                          int* n_defer,
                                                           unsigned long long seq) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -416,6 +417,7 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, cons
       __threadfence();
       const int st = atomicExch(status, 0);
       *ticket = 0u;
+      *n_defer = 0;  // the per-node fast path's deferred count, 0 at rest
       out[n_nodes] = (double)st;
       __threadfence_system();
       reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
@@ -468,6 +470,92 @@ __global__ __launch_bounds__(kBlock) void node_kernel(const double* x, const int
   if (COUNT) {
     double d = 0.0;
     block_reduce<COUNT>(d, zero, ne);
+    if (threadIdx.x == 0) atomicAdd(evals, (unsigned long long)ne);
+  }
+}
+
+// Two-pass per-node path (used when every node's parameters select the same
+// integration family, the usual HDDM case: sv/sz/st are group-level):
+// node_fast_kernel is fast_kernel with the node's parameter row (staged in
+// LDS as in node_kernel) and per-trial log p out; a trial that needs
+// refinement is appended — index and parameter row — to a dense deferred
+// list (wave-aggregated atomic; the order does not matter, outputs are per
+// trial), which node_slow_kernel runs 64 trials per wave.
+__device__ inline double node_logp(double p, const Params& Q, const Knobs& K) {
+  const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);  // wfpt.pyx:63-64 per node
+  p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
+  return (!ok || p == 0) ? -INFINITY : log(p);
+}
+
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
+                      double* lp, int64_t* d_idx, Params* d_par, int* n_defer,
+                      unsigned long long* evals) {
+  __shared__ Params rows[kStageRows];
+  const int64_t i0 = (int64_t)blockIdx.x * kBlock;
+  const int64_t i = i0 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int first = node[i0];
+  const int last = node[(i0 + kBlock - 1 < n) ? i0 + kBlock - 1 : n - 1];
+  const int span = last - first + 1;
+  const bool staged = span <= kStageRows;
+  if (staged) {
+    const double* src = reinterpret_cast<const double*>(P + first);
+    double* dst = reinterpret_cast<double*>(rows);
+    for (int k = threadIdx.x; k < span * 8; k += kBlock) dst[k] = src[k];
+  }
+  __syncthreads();
+  long long ne = 0;
+  bool slow = false;
+  Params Q;
+  if (i < n) {
+    const int nj = node[i];
+    Q = staged ? rows[nj - first] : P[nj];
+    int valid = 0;
+    const double p = fast_pdf<MODE>(x[i], Q, K, slow, valid);
+    if (!slow) {
+      if (COUNT && valid) ne = fast_evals(MODE);
+      lp[i] = node_logp(p, Q, K);
+    }
+  }
+  if (MODE != kDirect) {
+    const unsigned long long b = __ballot(slow);
+    if (b) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
+      base = __shfl(base, 0, 64);
+      if (slow) {
+        const int k = base + __popcll(b & ((1ull << lane) - 1ull));
+        d_idx[k] = i;
+        d_par[k] = Q;
+      }
+    }
+  }
+  if (COUNT) {
+    ne = wave_sum_ll(ne);
+    if (lane == 0) atomicAdd(evals, (unsigned long long)ne);
+  }
+}
+
+template <int MODE, int STK, bool COUNT>
+__global__ __launch_bounds__(64) void node_slow_kernel(const double* x, Knobs K, double* lp,
+                                                       const int64_t* d_idx, const Params* d_par,
+                                                       const int* n_defer,
+                                                       unsigned long long* evals, int* status) {
+  using Stack = typename StackOf<STK>::type;
+  const int nd = *n_defer;
+  long long ne = 0;
+  int ovf = 0;
+  for (int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x; k < nd; k += (int64_t)gridDim.x * 64) {
+    const int64_t i = d_idx[k];
+    const Params Q = d_par[k];
+    const double p = full_pdf<MODE, Stack, COUNT>(x[i], Q, K, ne, ovf);
+    lp[i] = node_logp(p, Q, K);
+  }
+  if (ovf) atomicOr(status, ovf);
+  if (COUNT) {
+    ne = wave_sum_ll(ne);
     if (threadIdx.x == 0) atomicAdd(evals, (unsigned long long)ne);
   }
 }
@@ -642,11 +730,57 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int* stat
                      seq);
 }
 
+template <int MODE, bool COUNT>
+static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t n,
+                                  const Params* P, const Knobs& K, double* lp, int64_t* d_idx,
+                                  Params* d_par, int* n_defer, unsigned long long* evals,
+                                  int* status, hipStream_t s) {
+  hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
+                     node, n, P, K, lp, d_idx, d_par, n_defer, evals);
+  if (MODE == kDirect) return;
+  const int64_t nl = (n + 63) / 64;
+  const int64_t g = nl < 2048 ? nl : 2048;
+  const int stk = stack_kind(K);
+  if (stk == 0)
+    hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
+                       d_idx, d_par, n_defer, evals, status);
+  else if (stk == 1)
+    hipLaunchKernelGGL((node_slow_kernel<MODE, 1, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
+                       d_idx, d_par, n_defer, evals, status);
+  else
+    hipLaunchKernelGGL((node_slow_kernel<MODE, 2, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
+                       d_idx, d_par, n_defer, evals, status);
+}
+
+template <bool COUNT>
+static void launch_nodes_mode(int mode, const double* x, const int32_t* node, int64_t n,
+                              const Params* P, const Knobs& K, double* lp, int64_t* d_idx,
+                              Params* d_par, int* n_defer, unsigned long long* evals,
+                              int* status, hipStream_t s) {
+#define TWO_PASS(M_) \
+  launch_nodes_two_pass<M_, COUNT>(x, node, n, P, K, lp, d_idx, d_par, n_defer, evals, status, s)
+  switch (mode) {
+    case kDirect: TWO_PASS(kDirect); break;
+    case kAdaptT: TWO_PASS(kAdaptT); break;
+    case kAdaptZ: TWO_PASS(kAdaptZ); break;
+    default: TWO_PASS(kAdaptTZ); break;
+  }
+#undef TWO_PASS
+}
+
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
-                  const Knobs& K, double* lp, unsigned long long* evals, int* status,
-                  hipStream_t s) {
+                  const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
+                  int* n_defer, unsigned long long* evals, int* status, hipStream_t s) {
   const int64_t nb = blocks_for(n);
   if (nb == 0) return;
+  if (mode >= kDirect && mode <= kAdaptTZ) {
+    if (evals)
+      launch_nodes_mode<true>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, evals, status, s);
+    else
+      launch_nodes_mode<false>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, evals, status,
+                               s);
+    return;
+  }
   const int stk = stack_kind(K);
 #define NODE_LAUNCH(S_, C_)                                                                  \
   hipLaunchKernelGGL((node_kernel<S_, C_>), dim3(nb), dim3(kBlock), 0, s, x, node, n, P, K, \
@@ -664,10 +798,11 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
 }
 
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
-                        int* status, unsigned* ticket, unsigned long long seq, hipStream_t s) {
+                        int* status, unsigned* ticket, int* n_defer, unsigned long long seq,
+                        hipStream_t s) {
   if (n_nodes <= 0) return;
   hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                     n_nodes, out, status, ticket, seq);
+                     n_nodes, out, status, ticket, n_defer, seq);
 }
 
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,

@@ -283,3 +283,43 @@ def test_gen_rts_from_cdf(gpu):
     assert np.all(np.abs(rts) >= 0.25)
     # P(upper) = prob_ub (pdf.pxi:67-72) = 0.731 for v=.5, a=2, z=.5
     assert abs(np.mean(rts > 0) - gpu.prob_ub(0.5, 2.0, 0.5)) < 0.02
+
+
+@pytest.mark.parametrize("family", ["full", "simple", "sz_only", "st_only"])
+def test_nodes_uniform_family_fast_path(gpu, oracle_lib, family):
+    """Every node selects the same integration family (the HDDM case: sv/sz/st
+    are group-level), so wfpt_wiener_like_nodes takes the two-pass per-node
+    fast path; per-node sums must match the reference per node."""
+    rng = np.random.default_rng(29)
+    n_nodes = 53
+    sizes = rng.integers(1, 300, n_nodes)
+    sizes[7] = 0  # an empty node between non-empty ones
+    node = np.repeat(np.arange(n_nodes), sizes)
+    rng.shuffle(node)
+    x = rng.choice([-1.0, 1.0], node.size) * (0.25 + rng.gamma(2.0, 0.4, node.size))
+    P = np.zeros((n_nodes, 8))
+    P[:, 0] = rng.uniform(-2, 2, n_nodes)
+    P[:, 2] = rng.uniform(0.8, 2.0, n_nodes)
+    P[:, 3] = rng.uniform(0.4, 0.6, n_nodes)
+    P[:, 5] = rng.uniform(0.2, 0.33, n_nodes)
+    P[:, 7] = 0.05
+    if family == "full":
+        P[:, 1], P[:, 4], P[:, 6] = 0.6, 0.25, 0.2  # wide sz/st: some trials refine (slow pass)
+    elif family == "sz_only":
+        P[:, 4] = 0.3
+    elif family == "st_only":
+        P[:, 6] = 0.25
+    P[3, 7] = 1.5    # out-of-range p_outlier => -inf for that node
+    P[5, 7] = 0.0    # no outliers: trials below t - st/2 give -inf
+    ds = gpu.Dataset(x, node_id=node, n_nodes=n_nodes)
+    got = ds.wiener_like_nodes(P, 1e-4, 2, 2, 1, 1e-3, 0.1)
+    for j in range(n_nodes):
+        xj = x[node == j]
+        v, sv, a, z, sz, t, st, po = P[j]
+        ref = oracle_lib.wiener_like(xj, v, sv, a, z, sz, t, st, 1e-4, 2, 2, 1, 1e-3, po, 0.1)
+        if not np.isfinite(ref):
+            assert got[j] == ref, (j, got[j], ref)
+        else:
+            terms = oracle_lib.pdf_array(xj, v, sv, a, z, sz, t, st, 1e-4, 1, 2, 2, 1, 1e-3, po,
+                                         0.1)
+            assert_total(got[j], terms, f"{family} node {j}")
