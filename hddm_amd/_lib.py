@@ -18,6 +18,14 @@ if not os.path.exists(LIB_PATH):
         f"hddm_amd: HIP library not found at {LIB_PATH}; build it with "
         "`python -m hddm_amd.build` (hipcc --offload-arch=gfx950)")
 
+# Kernel arguments in device memory: every wave of the likelihood kernels
+# reads its ~150-byte argument block with scalar loads at start; from the
+# default host-side kernarg pool those are PCIe round trips (measured on
+# MI355X: 2.5% of the full-DDM kernel time). Read by the HIP runtime when it
+# initialises, i.e. at the first call into the library; an explicit setting
+# wins.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+
 _lib = ctypes.CDLL(LIB_PATH)
 
 WFPT_OK = 0
