@@ -100,7 +100,6 @@ struct wfpt_ctx {
   DevBuf<int> zero;       // block zero counts
   DevBuf<double> res;     // final {sum, zeros} or per-node results
   DevBuf<double> lp;      // per-trial outputs
-  DevBuf<wfpt::Params> nodep;
   DevBuf<double> marr;    // wiener_like_multi parameter arrays
   DevBuf<double*> mptr;
   DevBuf<double> mscal;
@@ -113,8 +112,6 @@ struct wfpt_ctx {
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
-  double* host = nullptr;  // pinned result slot
-  size_t host_cap = 0;
   double* mres = nullptr;      // mapped pinned {sum, zeros, status}: finalize writes it
   double* mres_dev = nullptr;  // its device alias
   unsigned long long seq = 0;  // completion word finalize writes to mres[3]
@@ -183,14 +180,6 @@ wfpt::Knobs to_knobs(const wfpt_knobs* k) {
 
 bool p_outlier_in_range(double p) { return (p >= 0) & (p <= 1); }  // wfpt.pyx:50-51
 
-int ensure_host(wfpt_ctx* c, size_t n) {
-  if (n <= c->host_cap) return WFPT_OK;
-  if (c->host) (void)hipHostFree(c->host);
-  c->host = nullptr;
-  HIP_TRY(hipHostMalloc((void**)&c->host, n * sizeof(double), hipHostMallocDefault));
-  c->host_cap = n;
-  return WFPT_OK;
-}
 
 // Paths without finalize_kernel (pdf_array, nodes): clear the overflow flag
 // before the launch, copy it back (and clear it again) before the stream sync.
@@ -380,7 +369,6 @@ void wfpt_close(wfpt_ctx* c) {
   c->zero.release();
   c->res.release();
   c->lp.release();
-  c->nodep.release();
   c->marr.release();
   c->mptr.release();
   c->mscal.release();
@@ -393,7 +381,6 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
-  if (c->host) (void)hipHostFree(c->host);
   if (c->mres) (void)hipHostFree(c->mres);
   c->mnodep.release();
   c->mnode.release();
@@ -717,14 +704,15 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   HIP_TRY(c->res.reserve(3));
-  if (int rc = ensure_host(c, 3)) return rc;
   if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p)) return rc;
   // {sum, zeros, status} of every rank summed: any zero trial or failure anywhere
   // reaches every rank
   NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 3, ncclDouble, ncclSum, c->comm, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->host, c->res.p, 3 * sizeof(double), hipMemcpyDeviceToHost,
-                         c->stream));
-  return read_sum(c, c->host, out);
+  // the summed result goes to the mapped slot with a fresh completion word
+  // (run_sum's finalize used the previous one for the device copy)
+  wfpt::launch_publish(c->res.p, c->mres_dev, ++c->seq, c->stream);
+  HIP_TRY(hipGetLastError());
+  return read_sum(c, c->mres, out);
 }
 
 int wfpt_profile_enable(wfpt_ctx* c, int flags) {

@@ -21,6 +21,8 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
                    unsigned char* wl, int* wl_n, hipStream_t s);
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt);
+// res[0..2] (device) -> out[0..2] (mapped host), then out[3] = seq.
+void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
 // out[0..2] = {sum, #zero trials, status flags}, then out[3] = seq (as a
 // 64-bit word) once they are visible; resets *status to 0.
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,

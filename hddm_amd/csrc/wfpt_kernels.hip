@@ -380,6 +380,24 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
   }
 }
 
+// Copies a device result {sum, zeros, status} (after the RCCL all-reduce) to
+// the mapped host slot, then writes the completion word (as finalize_kernel).
+__global__ __launch_bounds__(64) void publish_kernel(const double* res, double* out,
+                                                     unsigned long long seq) {
+  if (threadIdx.x == 0) {
+    out[0] = res[0];
+    out[1] = res[1];
+    out[2] = res[2];
+    __threadfence_system();
+    reinterpret_cast<volatile unsigned long long*>(out)[3] = seq;
+    __threadfence_system();
+  }
+}
+
+void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s) {
+  hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, s, res, out, seq);
+}
+
 // One wave per node: sums per-trial log p of [off[j], off[j+1]) in fixed order.
 // out[j] = -inf if the node holds a zero-density trial (wfpt.pyx:71-72).
 // `out` is mapped pinned host memory: out[n_nodes] receives the call's status
