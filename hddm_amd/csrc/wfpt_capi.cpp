@@ -231,10 +231,12 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   if (int rc = reserve_worklist(c, n)) return rc;
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  // profiling: ev0..ev1 bracket the level-0 fast kernel (the dominant kernel,
+  // the one rocprofv3 reports as fast_kernel<...>)
   wfpt::launch_trials(0, dx, n, P, K, c->part.p, c->zero.p, c->count ? c->evals : nullptr,
-                      c->status, 0, c->wl.p, c->wl_n.p, c->stream);
+                      c->status, 0, c->wl.p, c->wl_n.p, c->stream,
+                      c->profile ? c->ev1 : nullptr);
   HIP_TRY(hipGetLastError());
-  if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   int64_t off = 0, cnt = 0;
   wfpt::final_partials(n, P, K, &off, &cnt);
   wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, out, ++c->seq,

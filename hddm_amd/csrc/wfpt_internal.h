@@ -16,9 +16,11 @@ int64_t blocks_for(int64_t n);
 // Adaptive modes run a level-0 fast pass then a slow pass over the deferred
 // trials: wl must hold blocks_for(n)*256 bytes and wl_n blocks_for(n) ints;
 // OUT_SUM then leaves partials_for(n) block partials in out/zeros.
+// fast_done (optional) is recorded right after the level-0 fast kernel.
 void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
                    double* out, int* zeros, unsigned long long* evals, int* status, int logp,
-                   unsigned char* wl, int* wl_n, hipStream_t s);
+                   unsigned char* wl, int* wl_n, hipStream_t s,
+                   hipEvent_t fast_done = nullptr);
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt);
 // res[0..2] (device) -> out[0..2] (mapped host), then out[3] = seq.

@@ -645,7 +645,7 @@ constexpr bool t_split(int mode) {
 
 template <int MODE, bool COUNT, int OUT>
 static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned char* wl,
-                            int* wl_n, hipStream_t s) {
+                            int* wl_n, hipStream_t s, hipEvent_t fast_done) {
   // both fast kernels leave one partial / worklist per 64 trials
   constexpr int TPB = 64;
   const int64_t nb = (n + TPB - 1) / TPB;
@@ -655,6 +655,7 @@ static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned cha
   else
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
                        A, wl, wl_n);
+  if (fast_done) (void)hipEventRecord(fast_done, s);
   if (MODE == kDirect) return;
   const int64_t g = slow_grid(nb);
   if (stk == 0)
@@ -670,24 +671,25 @@ static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned cha
 
 template <bool COUNT, int OUT>
 static void launch_out(int mode, int stk, const TrialArgs& A, int64_t nb, unsigned char* wl,
-                       int* wl_n, hipStream_t s) {
+                       int* wl_n, hipStream_t s, hipEvent_t ev) {
   switch (mode) {
-    case kDirect: launch_two_pass<kDirect, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
-    case kAdaptT: launch_two_pass<kAdaptT, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
-    case kAdaptZ: launch_two_pass<kAdaptZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
-    case kAdaptTZ: launch_two_pass<kAdaptTZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s); break;
+    case kDirect: launch_two_pass<kDirect, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
+    case kAdaptT: launch_two_pass<kAdaptT, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
+    case kAdaptZ: launch_two_pass<kAdaptZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
+    case kAdaptTZ: launch_two_pass<kAdaptTZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
     case kFixedT: launch_generic<kFixedT, 0, COUNT, OUT>(A, nb, s); break;
     case kFixedZ: launch_generic<kFixedZ, 0, COUNT, OUT>(A, nb, s); break;
     default: launch_generic<kFixedTZ, 0, COUNT, OUT>(A, nb, s); break;
   }
+  if (ev && mode > kAdaptTZ) (void)hipEventRecord(ev, s);  // the single trial kernel
 }
 
 template <bool COUNT>
 static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, int64_t nb,
-                         unsigned char* wl, int* wl_n, hipStream_t s) {
-  if (out_kind == OUT_SUM) launch_out<COUNT, OUT_SUM>(mode, stk, A, nb, wl, wl_n, s);
-  else if (out_kind == OUT_ARRAY) launch_out<COUNT, OUT_ARRAY>(mode, stk, A, nb, wl, wl_n, s);
-  else launch_out<COUNT, OUT_LOGP>(mode, stk, A, nb, wl, wl_n, s);
+                         unsigned char* wl, int* wl_n, hipStream_t s, hipEvent_t ev) {
+  if (out_kind == OUT_SUM) launch_out<COUNT, OUT_SUM>(mode, stk, A, nb, wl, wl_n, s, ev);
+  else if (out_kind == OUT_ARRAY) launch_out<COUNT, OUT_ARRAY>(mode, stk, A, nb, wl, wl_n, s, ev);
+  else launch_out<COUNT, OUT_LOGP>(mode, stk, A, nb, wl, wl_n, s, ev);
 }
 
 // Where launch_trials(OUT_SUM) leaves the partials finalize must sum: the
@@ -723,7 +725,7 @@ int64_t blocks_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
 void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
                    double* out, int* zeros, unsigned long long* evals, int* status, int logp,
-                   unsigned char* wl, int* wl_n, hipStream_t s) {
+                   unsigned char* wl, int* wl_n, hipStream_t s, hipEvent_t fast_done) {
   TrialArgs A;
   A.x = x;
   A.n = n;
@@ -738,8 +740,8 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   const int64_t nb = blocks_for(n);
   if (nb == 0) return;
-  if (evals) launch_count<true>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s);
-  else launch_count<false>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s);
+  if (evals) launch_count<true>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s, fast_done);
+  else launch_count<false>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s, fast_done);
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
