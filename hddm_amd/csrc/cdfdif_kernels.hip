@@ -340,7 +340,8 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
 
 }  // namespace
 
-// dmat_cdf_array on device x[n] (cdfdif_wrapper.pyx:16-53): par holds the
+// dmat_cdf_array on device x[n] (cdfdif_wrapper.pyx:16-53); *n_defer must be
+// 0 (the caller clears it on the stream). par holds the
 // wrapper's transformed parameters (a/10, t, sv/10+1e-10, z*a/10,
 // sz*a/10+1e-10, st+1e-10, v/10).
 void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
@@ -355,7 +356,6 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   P.st = par[5];
   P.nu = par[6];
   const int64_t nb = (n + kCdfBlock - 1) / kCdfBlock;
-  (void)hipMemsetAsync(n_defer, 0, sizeof(int), s);
   hipLaunchKernelGGL(dmat_cdf_kernel, dim3(nb), dim3(kCdfBlock), 0, s, x, n, P, p_outlier,
                      w_outlier, out, defer, n_defer);
   // one wave per deferred trial on a fixed grid (it reads the count itself)

@@ -651,6 +651,7 @@ int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_para
   HIP_TRY(c->lp.reserve(n));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   HIP_TRY(c->defer.reserve(n + 1));
+  HIP_TRY(hipMemsetAsync(c->defer.p + n, 0, sizeof(int), c->stream));
   wfpt::launch_dmat_cdf(c->x.p, n, par, po, w_outlier, c->lp.p, c->defer.p, c->defer.p + n,
                         c->stream);
   HIP_TRY(hipGetLastError());
