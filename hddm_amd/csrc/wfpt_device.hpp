@@ -133,10 +133,83 @@ struct TNode {
   int pos;      // xx > 0 (else density 0, pdf.pxi:92)
 };
 
+// Series branch and term count of one t node (pdf.pxi:36-60): small-time
+// series iff ks < kl, K = ceil(min). kl and ks feed ONLY these two decisions.
+struct Decision {
+  int small, K;
+};
+
+// fp32 estimate of the decision (~1e-7 relative). Returns false — the caller
+// must then run the reference's fp64 operations — when any decision is within
+// 1e-5 (relative) of flipping or an fp32 argument is out of range. args_out:
+// the small-time log argument 2 sqrt(2 pi tt) err (for the monotonicity test
+// of shared decisions).
+__device__ inline bool decide32(double tt, double err, Decision& D, float& args_out) {
+  args_out = 2.0f;
+  if (!(tt > 1e-30 && tt < 1e30 && err > 1e-30 && err < 1e30)) return false;
+  const float ttf = (float)tt, errf = (float)err;
+  const float sqtf = sqrtf(ttf);
+  const float ipsf = 1.0f / ((float)kPi * sqtf);
+  const float argl = ((float)kPi * ttf) * errf;
+  const float args = (2.0f * sqrtf((2.0f * (float)kPi) * ttf)) * errf;
+  args_out = args;
+  const bool use_l = argl < 1.0f;
+  const bool use_s = args < 1.0f;
+  const float tol = 1e-5f;
+  // |dL| <~ 2e-7 from fp32 rounding + logf; the relative error it induces in
+  // kl/ks is <= |dL| / (2|L|), so |L| >= 0.1 keeps it <= 1e-6 (10x inside tol).
+  const float Ll = use_l ? logf(argl) : -1.0f;
+  const float Ls = use_s ? logf(args) : -1.0f;
+  float klf = use_l ? sqrtf((-2.0f * Ll) / ((float)kPi2 * ttf)) : ipsf;
+  float ksf = use_s ? 2.0f + sqrtf((-2.0f * ttf) * Ls) : 2.0f;
+  const float b2 = sqtf + 1.0f;
+  const bool amb_t = fabsf(argl - 1.0f) <= tol || fabsf(args - 1.0f) <= tol;
+  const bool amb_l = use_l && fabsf(klf - ipsf) <= tol * klf;
+  const bool amb_s = use_s && fabsf(ksf - b2) <= tol * ksf;
+  if (use_l) klf = (klf < ipsf) ? ipsf : klf;
+  if (use_s) ksf = (ksf < b2) ? b2 : ksf;
+  const float kk = (ksf < klf) ? ksf : klf;
+  const bool amb_b = fabsf(ksf - klf) <= tol * klf;
+  const bool amb_k = fabsf(kk - rintf(kk)) <= tol * kk;
+  const bool rng = (use_l && !(argl > 1e-30f)) || (use_s && !(args > 1e-30f));
+  if (rng || Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k) return false;
+  D.small = ksf < klf;
+  D.K = (int)ceilf(kk);
+  return true;
+}
+
+// The reference's fp64 operations (pdf.pxi:36-60).
+__device__ inline Decision decide64(double tt, double err) {
+  double kl, ks;
+  const double sqt = sqrt(tt);
+  const double inv_pi_sqt = 1. / (kPi * sqt);
+  const double arg_l = (kPi * tt) * err;
+  const double arg_s = (2.0 * sqrt((2.0 * kPi) * tt)) * err;
+  if (arg_l < 1.0) {
+    kl = sqrt((-2.0 * log(arg_l)) / (kPi2 * tt));
+    kl = (kl < inv_pi_sqt) ? inv_pi_sqt : kl;
+  } else {
+    kl = inv_pi_sqt;
+  }
+  if (arg_s < 1.0) {
+    ks = 2.0 + sqrt((-2.0 * tt) * log(arg_s));
+    const double b = sqt + 1.0;
+    ks = (ks < b) ? b : ks;
+  } else {
+    ks = 2.0;
+  }
+  Decision D;
+  D.small = ks < kl;
+  D.K = (int)ceil(D.small ? ks : kl);
+  return D;
+}
+
 // qhint >= 0: exp(-pi^2 tt / 2) of this node computed by the caller (a
-// recurrence over the t grid); < 0: computed here.
+// recurrence over the t grid); < 0: computed here. has_known: `known` is the
+// node's decision, established by the caller (shared over a trial's t grid).
 __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err,
-                                    double qhint = -1.0) {
+                                    double qhint = -1.0, bool has_known = false,
+                                    Decision known = Decision{0, 0}) {
   TNode T;
   T.xx = xx;
   T.pos = xx > 0;
@@ -153,67 +226,13 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   const double a2 = a * a;
   const double tt = xx / a2;
   T.tt = tt;
-  // Series branch and term count (pdf.pxi:36-60). kl and ks feed ONLY these
-  // two decisions, so they are first computed with fp32 logs (~1e-7 abs.);
-  // when any decision is within 1e-5 of flipping — or an fp32 argument is out
-  // of range — they are recomputed with the reference's fp64 operations.
-  // fp32 estimate of every decision input; the fp64 reference operations run
-  // only for lanes where a decision is within 1e-5 (relative) of flipping or an
-  // input is outside the fp32 range.
-  double kl = 0.0, ks = 0.0;
-  bool use_l = false, use_s = false;
-  bool exact = WFPT_EXACT_MATH || !(tt > 1e-30 && tt < 1e30 && err > 1e-30 && err < 1e30);
-  if (!exact) {
-    const float ttf = (float)tt, errf = (float)err;
-    const float sqtf = sqrtf(ttf);
-    const float ipsf = 1.0f / ((float)kPi * sqtf);
-    const float argl = ((float)kPi * ttf) * errf;
-    const float args = (2.0f * sqrtf((2.0f * (float)kPi) * ttf)) * errf;
-    use_l = argl < 1.0f;
-    use_s = args < 1.0f;
-    const float tol = 1e-5f;
-    // |dL| <~ 2e-7 from fp32 rounding + logf; the relative error it induces in
-    // kl/ks is <= |dL| / (2|L|), so |L| >= 0.1 keeps it <= 1e-6 (10x inside tol).
-    const float Ll = use_l ? logf(argl) : -1.0f;
-    const float Ls = use_s ? logf(args) : -1.0f;
-    float klf = use_l ? sqrtf((-2.0f * Ll) / ((float)kPi2 * ttf)) : ipsf;
-    float ksf = use_s ? 2.0f + sqrtf((-2.0f * ttf) * Ls) : 2.0f;
-    const float b2 = sqtf + 1.0f;
-    const bool amb_t = fabsf(argl - 1.0f) <= tol || fabsf(args - 1.0f) <= tol;
-    const bool amb_l = use_l && fabsf(klf - ipsf) <= tol * klf;
-    const bool amb_s = use_s && fabsf(ksf - b2) <= tol * ksf;
-    if (use_l) klf = (klf < ipsf) ? ipsf : klf;
-    if (use_s) ksf = (ksf < b2) ? b2 : ksf;
-    const float kk = (ksf < klf) ? ksf : klf;
-    const bool amb_b = fabsf(ksf - klf) <= tol * klf;
-    const bool amb_k = fabsf(kk - rintf(kk)) <= tol * kk;
-    const bool rng = (use_l && !(argl > 1e-30f)) || (use_s && !(args > 1e-30f));
-    exact = rng || Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k;
-    kl = klf;
-    ks = ksf;
-  }
-  if (exact) {  // the reference's fp64 operations, pdf.pxi:36-47
-    const double sqt = sqrt(tt);
-    const double inv_pi_sqt = 1. / (kPi * sqt);
-    const double arg_l = (kPi * tt) * err;
-    const double arg_s = (2.0 * sqrt((2.0 * kPi) * tt)) * err;
-    if (arg_l < 1.0) {
-      kl = sqrt((-2.0 * log(arg_l)) / (kPi2 * tt));
-      kl = (kl < inv_pi_sqt) ? inv_pi_sqt : kl;
-    } else {
-      kl = inv_pi_sqt;
-    }
-    if (arg_s < 1.0) {
-      ks = 2.0 + sqrt((-2.0 * tt) * log(arg_s));
-      const double b = sqt + 1.0;
-      ks = (ks < b) ? b : ks;
-    } else {
-      ks = 2.0;
-    }
-  }
-  if (ks < kl) {
+  Decision D;
+  float args;
+  if (has_known) D = known;
+  else if (WFPT_EXACT_MATH || !decide32(tt, err, D, args)) D = decide64(tt, err);
+  if (D.small) {
     T.small = 1;
-    T.K = (int)ceil(ks);
+    T.K = D.K;
 #if WFPT_EXACT_MATH
     T.rn = 1.0 / sqrt((2.0 * kPi) * ((tt * tt) * tt));
 #else
@@ -222,7 +241,7 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
     T.m = -0.5 / tt;
   } else {
     T.small = 0;
-    T.K = (int)ceil(kl);
+    T.K = D.K;
     T.m = qhint >= 0.0 ? qhint : exp((-kPi2 * tt) / 2.0);
     T.q2 = T.m * T.m;
   }
@@ -964,12 +983,28 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
       qn[4] = q0 * (R2 * R);   // e
     }
   }
+  // Shared series decision: ks(tt) increases and kl(tt) decreases with tt
+  // (pdf.pxi:36-47; ks only while its log argument stays below e^-1/2, hence
+  // the 0.5 test at the largest tt), so when the outermost t nodes (largest /
+  // smallest tt) take the same branch and K with both fp32 decisions clear of
+  // every threshold, all 5 nodes do. Otherwise each node decides itself.
+  // (The two end decisions also serve their own nodes, j = 0 and 1.)
+  Decision D0{0, 0}, D1{0, 0};
+  bool ok0 = false, ok1 = false, shared = false;
+  if (!WFPT_EXACT_MATH && x - ub > 0) {
+    const double a2 = a * a;
+    float args0, args1;
+    ok0 = decide32((x - lb) / a2, err, D0, args0);
+    ok1 = decide32((x - ub) / a2, err, D1, args1);
+    shared = ok0 && ok1 && args0 < 0.5f && D0.small == D1.small && D0.K == D1.K;
+  }
   double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
 #pragma unroll 1
   for (int j = 0; j < 5; ++j) {
     const double tc = j == 0 ? lb : j == 1 ? ub : j == 2 ? c : j == 3 ? d : e;
     const double qh = j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
-    const TNode T = tnode_setup(x - tc, v, sv, a, err, qh);
+    const bool known = j == 0 ? ok0 : (j == 1 ? ok1 : shared);
+    const TNode T = tnode_setup(x - tc, v, sv, a, err, qh, known, j == 1 ? D1 : D0);
     double y;
     if (MODE == kAdaptTZ) {
       y = level0_z(T, G, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
