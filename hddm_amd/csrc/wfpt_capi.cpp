@@ -117,7 +117,6 @@ struct wfpt_ctx {
   unsigned long long seq = 0;  // completion word finalize writes to mres[3]
   MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
   MappedBuf<double> mnode;         // per-node sums + status + completion word
-  unsigned* ticket = nullptr;      // device: last-block counter of segment_sum_kernel
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
   bool profile = false;      // HIP events around the main kernel
@@ -349,8 +348,6 @@ int wfpt_open(int device, wfpt_ctx** out) {
     e = hipHostMalloc((void**)&c->mres, 4 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->ticket, sizeof(unsigned));
-  if (e == hipSuccess) e = hipMemset(c->ticket, 0, sizeof(unsigned));
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
   if (e != hipSuccess) {
@@ -386,7 +383,7 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->mres) (void)hipHostFree(c->mres);
   c->mnodep.release();
   c->mnode.release();
-  if (c->ticket) (void)hipFree(c->ticket);
+
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -556,9 +553,11 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   }
   if (mode > wfpt::kAdaptTZ) mode = -1;  // fixed Simpson: generic kernel
   if (c->nodes_generic) mode = -1;
+  HIP_TRY(c->res.reserve(std::max<int32_t>(m, 1)));
   if (mode >= 0) {  // deferred-trial records of the per-node fast path
     HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
+    HIP_TRY(hipMemsetAsync(c->n_defer, 0, sizeof(int), c->stream));
   }
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
@@ -572,8 +571,8 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   ++c->seq;
   if (m > 0) {
     // per-node sums, status and the completion word land in mapped memory
-    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->mnode.d, c->status, c->ticket, c->n_defer,
-                             c->seq, c->stream);
+    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->mnode.d, c->status, c->seq,
+                             c->stream);
     HIP_TRY(hipGetLastError());
     if (int rc = wait_word(c, c->mnode.h + m + 1)) return rc;
     if (int rc = check_status_value(c->mnode.h[m])) return rc;

@@ -1029,66 +1029,6 @@ __device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, boo
   return S2 + (S2 - S) / 15;
 }
 
-// Outer-t split of the fast path (kAdaptT / kAdaptTZ): one lane evaluates ONE
-// of the 5 root-level t nodes of a trial (j = 0..4: lb, ub, mid, d, e of
-// integrate.pxi:132/144 -> 72-112/143-178), the 5 values are combined by
-// fast_t_combine. Returns f_j (already divided by the t range) and sets slow
-// when the node's inner z integral wants refinement.
-struct TrialPrep {
-  double x, v, z, st, sz;  // flipped and |x| (pdf.pxi:116-125)
-  int valid;
-};
-
-__device__ inline TrialPrep prepare_trial(double x, const Params& P) {
-  TrialPrep R;
-  const double a = P.a, sv = P.sv, t = P.t;
-  double v = P.v, z = P.z, st = P.st, sz = P.sz;
-  R.valid = !((z < 0) || (z > 1) || (a < 0) || (t < 0) || (st < 0) || (sv < 0) || (sz < 0) ||
-              (sz > 1) || ((fabs(x) - (t - st / 2.)) < 0) || (z + sz / 2. > 1) ||
-              (z - sz / 2. < 0) || (t - st / 2. < 0));
-  if (x > 0) {
-    v = -v;
-    z = 1. - z;
-  }
-  R.x = fabs(x);
-  R.v = v;
-  R.z = z;
-  R.st = (st < 1e-3) ? 0.0 : st;
-  R.sz = (sz < 1e-3) ? 0.0 : sz;
-  return R;
-}
-
-template <int MODE>
-__device__ inline double fast_t_node(const TrialPrep& R, int j, const Params& P, const Knobs& K,
-                                     bool& slow) {
-  const double a = P.a, sv = P.sv, t = P.t;
-  const double lb = t - R.st / 2., ub = t + R.st / 2.;
-  const double c = (ub + lb) / 2.;
-  const double tc = j == 0 ? lb : j == 1 ? ub : j == 2 ? c : j == 3 ? (lb + c) / 2. : (c + ub) / 2.;
-  const double iZt = 1.0 / (ub - lb);
-  const TNode T = tnode_setup(R.x - tc, R.v, sv, a, K.err);
-  if (MODE == kAdaptTZ) {
-    const double lbz = R.z - R.sz / 2., ubz = R.z + R.sz / 2.;
-    const ZGrid G = zgrid_setup(lbz, ubz, R.v, sv, a);
-    return level0_z(T, G, 1.0 / (ubz - lbz), K.simps_err, K.n_sz, R.v, sv, a, slow) * iZt;
-  }
-  return tnode_pdf_sv(T, R.z, R.v, sv, a) * iZt;
-}
-
-// Root aux node of the outer t integral from the 5 node values.
-__device__ inline double fast_t_combine(double f0, double f1, double f2, double f3, double f4,
-                                        const TrialPrep& R, const Params& P, const Knobs& K,
-                                        bool& slow) {
-  const double lb = P.t - R.st / 2., ub = P.t + R.st / 2.;
-  const double h = ub - lb;
-  const double S = (h / 6) * ((f0 + (4 * f2)) + f1);
-  const double Sl = (h / 12) * ((f0 + (4 * f3)) + f2);
-  const double Sr = (h / 12) * ((f2 + (4 * f4)) + f1);
-  const double S2 = Sl + Sr;
-  if (!(K.n_st <= 0 || fabs(S2 - S) <= 15 * K.simps_err)) slow = true;
-  return S2 + (S2 - S) / 15;
-}
-
 // evaluations of a trial that finished on the fast path (for W_trial counting)
 __host__ __device__ inline int fast_evals(int mode) {
   return mode == kDirect ? 1 : (mode == kAdaptTZ ? 25 : 5);

@@ -31,16 +31,15 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int* stat
                      unsigned long long seq, hipStream_t s);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
 // two-pass fast path; d_idx / d_par hold up to n deferred trials, *n_defer
-// is 0 at rest and reset by launch_segment_sum), or -1 (mixed / fixed
+// must be 0 on the stream), or -1 (mixed / fixed
 // Simpson: one generic per-trial kernel with a per-lane mode).
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
                   int* n_defer, unsigned long long* evals, int* status, hipStream_t s);
-// out (mapped host): [0, n_nodes) per-node sums, [n_nodes] status flags,
-// [n_nodes + 1] the 64-bit completion word seq (ticket: device counter, 0 at rest).
-void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
-                        int* status, unsigned* ticket, int* n_defer, unsigned long long seq,
-                        hipStream_t s);
+// res (device, n_nodes) per-node sums; then out (mapped host): [0, n_nodes)
+// the sums, [n_nodes] status flags, [n_nodes + 1] the 64-bit completion word.
+void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
+                        double* out, int* status, unsigned long long seq, hipStream_t s);
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
                   const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
                   hipStream_t s);

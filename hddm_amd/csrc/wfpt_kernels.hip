@@ -32,16 +32,6 @@ template <int MODE>
 struct FastWaves {
   static constexpr int value = MODE == kAdaptTZ ? WFPT_FAST_WAVES_TZ : WFPT_FAST_WAVES;
 };
-// outer-t split kernel: 320-thread blocks (5 waves); min waves per SIMD knob
-#ifndef WFPT_FAST_T_WAVES
-#define WFPT_FAST_T_WAVES 0
-#endif
-#if WFPT_FAST_T_WAVES > 0
-#define WFPT_FAST_T_BOUNDS __launch_bounds__(320, WFPT_FAST_T_WAVES)
-#else
-#define WFPT_FAST_T_BOUNDS __launch_bounds__(320)
-#endif
-
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
 
 __device__ inline double wave_sum(double v) {
@@ -183,67 +173,6 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
       if (OUT == OUT_SUM) {
         A.out[wave] = lp;
         A.zeros[wave] = zs;
-      }
-      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
-    }
-  }
-}
-
-// Outer-t split fast pass (kAdaptT, kAdaptTZ): a block of 5 waves owns 64
-// consecutive trials; wave j evaluates t node j of every trial (t-node-major,
-// so each wave sees one |rt|-sorted run and one series branch), the node values
-// meet in LDS and wave 0 finishes the outer Simpson step, the mixture, the log
-// and the block partial. Deferred trials go to wl/wl_n with 64 slots per block.
-constexpr int kTpb = 64;  // trials per outer-t block
-
-template <int MODE, bool COUNT, int OUT>
-__global__ WFPT_FAST_T_BOUNDS void fast_t_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
-  __shared__ double F[5][kTpb];
-  __shared__ int SL[5][kTpb];
-  const int lane = threadIdx.x & 63, j = threadIdx.x >> 6;
-  const int64_t i = (int64_t)blockIdx.x * kTpb + lane;
-  const bool in = i < A.n;
-  const double xi = in ? A.x[i] : 0.0;
-  const TrialPrep R = prepare_trial(xi, A.P);
-  bool slow = false;
-  double f = 0.0;
-  if (in && R.valid) f = fast_t_node<MODE>(R, j, A.P, A.K, slow);
-  F[j][lane] = f;
-  SL[j][lane] = slow;
-  __syncthreads();
-  if (j != 0) return;
-  slow = (SL[0][lane] | SL[1][lane] | SL[2][lane] | SL[3][lane] | SL[4][lane]) != 0;
-  double p = 0.0;
-  if (in && R.valid && !slow)
-    p = fast_t_combine(F[0][lane], F[1][lane], F[2][lane], F[3][lane], F[4][lane], R, A.P, A.K,
-                       slow);
-  slow = slow && in && R.valid;
-  long long ne = (COUNT && in && R.valid && !slow) ? fast_evals(MODE) : 0;
-  double lp = 0.0;
-  int zero = 0;
-  if (in && !slow) {
-    if (OUT == OUT_ARRAY) {
-      p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
-      A.out[i] = A.logp ? log(p) : p;
-    } else {
-      p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
-      if (p == 0) zero = 1;
-      else lp = log(p);
-      if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
-    }
-  }
-  const unsigned long long b = __ballot(slow);
-  if (slow) wl[(int64_t)blockIdx.x * kTpb + __popcll(b & ((1ull << lane) - 1ull))] =
-      (unsigned char)lane;
-  if (lane == 0) wl_n[blockIdx.x] = __popcll(b);
-  if (OUT == OUT_SUM || COUNT) {
-    lp = wave_sum(lp);
-    const int zs = __popcll(__ballot(zero != 0));
-    if (COUNT) ne = wave_sum_ll(ne);
-    if (lane == 0) {
-      if (OUT == OUT_SUM) {
-        A.out[blockIdx.x] = lp;
-        A.zeros[blockIdx.x] = zs;
       }
       if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
     }
@@ -399,48 +328,39 @@ void launch_publish(const double* res, double* out, unsigned long long seq, hipS
 }
 
 // One wave per node: sums per-trial log p of [off[j], off[j+1]) in fixed order.
-// out[j] = -inf if the node holds a zero-density trial (wfpt.pyx:71-72).
-// `out` is mapped pinned host memory: out[n_nodes] receives the call's status
-// flags and, once every block's results are visible, the 64-bit completion
-// word `seq` goes to out[n_nodes + 1] (written by the last block to finish,
-// found with a device-scope ticket counter that it resets for the next call).
+// res[j] = -inf if the node holds a zero-density trial (wfpt.pyx:71-72).
 __global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, const int64_t* off,
-                                                          int32_t n_nodes, double* out,
-                                                          int* status, unsigned* ticket,
-                                                          int* n_defer,
-                                                          unsigned long long seq) {
+                                                          int32_t n_nodes, double* res) {
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (j < n_nodes) {
-    const int64_t lo = off[j], hi = off[j + 1];
-    double s = 0.0;
-    int zero = 0;
-    for (int64_t i = lo + lane; i < hi; i += 64) {
-      const double v = lp[i];
-      if (v == -INFINITY) zero = 1;
-      else s += v;
-    }
-    s = wave_sum(s);
-    const bool anyz = __ballot(zero != 0) != 0ull;
-    if (lane == 0) {
-      out[j] = anyz ? -INFINITY : s;
-      __threadfence_system();
-    }
+  if (j >= n_nodes) return;
+  const int64_t lo = off[j], hi = off[j + 1];
+  double s = 0.0;
+  int zero = 0;
+  for (int64_t i = lo + lane; i < hi; i += 64) {
+    const double v = lp[i];
+    if (v == -INFINITY) zero = 1;
+    else s += v;
   }
+  s = wave_sum(s);
+  const bool anyz = __ballot(zero != 0) != 0ull;
+  if (lane == 0) res[j] = anyz ? -INFINITY : s;
+}
+
+// One block: copies the per-node sums to the mapped host slot, then the
+// call's status flags (out[n]) and, once all of it is visible, the 64-bit
+// completion word (out[n + 1]); resets the device status word.
+__global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, int32_t n,
+                                                            int* status, double* out,
+                                                            unsigned long long seq) {
+  for (int j = threadIdx.x; j < n; j += 256) out[j] = res[j];
+  __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
+    out[n] = (double)atomicExch(status, 0);
     __threadfence_system();
-    const unsigned t = atomicAdd(ticket, 1u);
-    if (t == gridDim.x - 1) {
-      __threadfence();
-      const int st = atomicExch(status, 0);
-      *ticket = 0u;
-      *n_defer = 0;  // the per-node fast path's deferred count, 0 at rest
-      out[n_nodes] = (double)st;
-      __threadfence_system();
-      reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
-      __threadfence_system();
-    }
+    reinterpret_cast<volatile unsigned long long*>(out + n + 1)[0] = seq;
+    __threadfence_system();
   }
 }
 
@@ -633,28 +553,14 @@ static void launch_generic(const TrialArgs& A, int64_t nb, hipStream_t s) {
 }
 
 // fast pass + (for adaptive modes) the slow pass on the deferred trials
-// Outer-t split (fast_t_kernel) is a build knob: on MI355X it measured
-// 0.35-0.47 ms vs 0.254-0.267 ms per 1M full-DDM trials for the per-trial
-// fast kernel (5-wave blocks, lower resident waves), so it is off by default.
-#ifndef WFPT_T_SPLIT
-#define WFPT_T_SPLIT 0
-#endif
-constexpr bool t_split(int mode) {
-  return WFPT_T_SPLIT && (mode == kAdaptT || mode == kAdaptTZ);
-}
-
 template <int MODE, bool COUNT, int OUT>
 static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned char* wl,
                             int* wl_n, hipStream_t s, hipEvent_t fast_done) {
   // both fast kernels leave one partial / worklist per 64 trials
   constexpr int TPB = 64;
   const int64_t nb = (n + TPB - 1) / TPB;
-  if (t_split(MODE))
-    hipLaunchKernelGGL((fast_t_kernel<MODE, COUNT, OUT>), dim3(nb), dim3(5 * kTpb), 0, s, A, wl,
-                       wl_n);
-  else
-    hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
-                       A, wl, wl_n);
+  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
+                     A, wl, wl_n);
   if (fast_done) (void)hipEventRecord(fast_done, s);
   if (MODE == kDirect) return;
   const int64_t g = slow_grid(nb);
@@ -817,12 +723,13 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
 #undef NODE_LAUNCH
 }
 
-void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* out,
-                        int* status, unsigned* ticket, int* n_defer, unsigned long long seq,
-                        hipStream_t s) {
+void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
+                        double* out, int* status, unsigned long long seq, hipStream_t s) {
   if (n_nodes <= 0) return;
   hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                     n_nodes, out, status, ticket, n_defer, seq);
+                     n_nodes, res);
+  hipLaunchKernelGGL(publish_nodes_kernel, dim3(1), dim3(256), 0, s, res, n_nodes, status, out,
+                     seq);
 }
 
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,

@@ -7,6 +7,7 @@ a relative tolerance, because the reference sums sequentially and the GPU sums
 by a fixed tree (SURVEY.md §7 hard part 5).
 """
 import math
+import zlib
 
 import numpy as np
 import pytest
@@ -35,7 +36,7 @@ def assert_density_parity(gpu, ref, what=""):
     tiny = pos & ~normal
     assert np.all(np.abs(gpu[tiny] - ref[tiny]) < 1e-300)
     sub = pos & (ref < np.finfo(np.float64).tiny)
-    assert np.all(np.abs(gpu[sub] - ref[sub]) <= SUBNORMAL_ATOL), f"{what}: subnormal"
+    assert np.all(np.abs(gpu[sub] - ref[sub]) <= subnormal_tol(ref[sub])), f"{what}: subnormal"
 
     neg = (ref < 0) & ~nan_r  # the large-t series can go (slightly) negative
     if neg.any():
@@ -46,10 +47,17 @@ LOG_DBL_MIN = np.log(np.finfo(np.float64).tiny)  # -708.4
 SUBNORMAL_ATOL = 8 * 4.9406564584124654e-324     # 8 subnormal ulps
 
 
+def subnormal_tol(p):
+    """|dp| allowed for a reference density p below DBL_MIN: the north_star's
+    |d log p| < 1e-6 (i.e. 1e-6 relative) or, deep in the subnormal range where
+    the reference's own value is quantised coarser than that, 8 subnormal ulps."""
+    return np.maximum(SUBNORMAL_ATOL, LOGP_TOL * np.abs(p))
+
+
 def assert_logp_parity(gpu, ref, what=""):
     """|dlogp| < 1e-6 per trial. A density below DBL_MIN is quantised to the
     subnormal grid (relative spacing up to 1e-5 near 1e-319) in the reference
-    itself, so there parity is |dp| <= 8 subnormal ulps."""
+    itself, so there parity is |dp| <= max(8 subnormal ulps, 1e-6 p)."""
     gpu = np.asarray(gpu, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     assert np.array_equal(np.isnan(gpu), np.isnan(ref)), f"{what}: NaN pattern"
@@ -60,7 +68,8 @@ def assert_logp_parity(gpu, ref, what=""):
     d = np.abs(gpu[nrm] - ref[nrm])
     assert d.size == 0 or d.max() < LOGP_TOL, f"{what}: max |dlogp| = {d.max():.3e}"
     ds = np.abs(np.exp(gpu[sub]) - np.exp(ref[sub]))
-    assert ds.size == 0 or ds.max() <= SUBNORMAL_ATOL, f"{what}: subnormal |dp| {ds.max()}"
+    ok = ds <= subnormal_tol(np.exp(ref[sub]))
+    assert ok.all(), f"{what}: subnormal |dp| {ds.max()}"
 
 
 def assert_total(gpu, ref_terms, what=""):
@@ -145,7 +154,7 @@ FAMILIES = {
 
 @pytest.mark.parametrize("fam", list(FAMILIES))
 def test_oracle_random_families(gpu, oracle_lib, fam):
-    rng = np.random.default_rng(hash(fam) % 2**32)
+    rng = np.random.default_rng(zlib.crc32(fam.encode()))
     for rep in range(6):
         p = dict(v=rng.uniform(-4, 4), a=rng.uniform(0.5, 2), t=rng.uniform(0.2, 0.5),
                  z=rng.uniform(0.4, 0.6), sv=rng.uniform(0, 2.5), sz=rng.uniform(0, 0.4),
