@@ -32,6 +32,18 @@ template <int MODE>
 struct FastWaves {
   static constexpr int value = MODE == kAdaptTZ ? WFPT_FAST_WAVES_TZ : WFPT_FAST_WAVES;
 };
+// Minimum waves per SIMD of the general (recursive) deferred-trial kernels:
+// left free their register use reaches 255 VGPRs + 2 AGPRs, one past the
+// 2-wave budget (1 wave / SIMD); 2 keeps them at 256 with a little more scratch.
+#ifndef WFPT_SLOW_WAVES
+#define WFPT_SLOW_WAVES 2
+#endif
+// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
+// occupy (256 CUs x 4 SIMDs x WFPT_SLOW_WAVES).
+#ifndef WFPT_SLOW_GRID
+#define WFPT_SLOW_GRID 2048
+#endif
+
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
 
 __device__ inline double wave_sum(double v) {
@@ -191,10 +203,10 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
 // into its own (lane j takes list g + jG of each 64-list chunk) and writes
 // A.out[nb + g] / A.zeros[nb + g]: finalize then sums G values. Fixed order
 // for a given n.
-constexpr int64_t kSlowGrid = 1024;
+constexpr int64_t kSlowGrid = WFPT_SLOW_GRID;
 
 template <int MODE, int STK, bool COUNT, int OUT>
-__global__ __launch_bounds__(64) void slow_kernel(TrialArgs A, const unsigned char* wl,
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void slow_kernel(TrialArgs A, const unsigned char* wl,
                                                   const int* wl_n, int64_t nl, int64_t nb) {
   using Stack = typename StackOf<STK>::type;
   long long ne = 0;
@@ -477,7 +489,7 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
 }
 
 template <int MODE, int STK, bool COUNT>
-__global__ __launch_bounds__(64) void node_slow_kernel(const double* x, Knobs K, double* lp,
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(const double* x, Knobs K, double* lp,
                                                        const int64_t* d_idx, const Params* d_par,
                                                        const int* n_defer,
                                                        unsigned long long* evals, int* status) {
