@@ -32,7 +32,8 @@ template <int MODE>
 struct FastWaves {
   static constexpr int value = MODE == kAdaptTZ ? WFPT_FAST_WAVES_TZ : WFPT_FAST_WAVES;
 };
-// Minimum waves per SIMD of the general (recursive) deferred-trial kernels:
+// Minimum waves per SIMD of the general (recursive) kernels (slow pass, generic
+// per-trial / per-node / per-trial-parameter kernels):
 // left free their register use reaches 255 VGPRs + 2 AGPRs, one past the
 // 2-wave budget (1 wave / SIMD); 2 keeps them at 256 with a little more scratch.
 #ifndef WFPT_SLOW_WAVES
@@ -109,7 +110,7 @@ struct StackOf<2> {
 };
 
 template <int MODE, int STK, bool COUNT, int OUT>
-__global__ __launch_bounds__(kBlock) void trial_kernel(TrialArgs A) {
+__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArgs A) {
   using Stack = typename StackOf<STK>::type;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   long long ne = 0;
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
 constexpr int kStageRows = 256;
 
 template <int STK, bool COUNT>
-__global__ __launch_bounds__(kBlock) void node_kernel(const double* x, const int32_t* node,
+__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(const double* x, const int32_t* node,
                                                       int64_t n, const Params* P, Knobs K,
                                                       double* lp, unsigned long long* evals,
                                                       int* status) {
@@ -512,7 +513,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(const do
 
 // wiener_like_multi (wfpt.pyx:244-274): per-trial parameters, ±999 = missing.
 template <int STK>
-__global__ __launch_bounds__(kBlock) void multi_kernel(const double* x, int64_t n,
+__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(const double* x, int64_t n,
                                                        const double* const* arr,
                                                        const double* scal, Knobs K,
                                                        double p_outlier, double* out,
