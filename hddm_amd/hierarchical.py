@@ -44,14 +44,19 @@ WIENER_PARAMS = {"err": 1e-4, "n_st": 2, "n_sz": 2, "use_adaptive": 1, "simps_er
 
 # ---------------------------------------------------------------- log densities
 
+_TINY = np.finfo(np.float64).tiny
+
+
 def gamma_logpdf_mean_sd(x, mean, sd):
     """pm.Gamma(alpha=mean^2/sd^2, beta=mean/sd^2) (base.py:642-667)."""
     x = np.asarray(x, dtype=np.float64)
     shape = mean ** 2 / sd ** 2
     rate = mean / sd ** 2
-    with np.errstate(divide="ignore", invalid="ignore"):
-        out = shape * np.log(rate) - special.gammaln(shape) + (shape - 1) * np.log(x) - rate * x
-    return np.where(x > 0, out, -np.inf)
+    pos = x > 0
+    # log of a clamped copy: no floating-point warnings to silence per call
+    out = shape * np.log(rate) - special.gammaln(shape) + (shape - 1) * np.log(
+        np.where(pos, x, _TINY)) - rate * x
+    return np.where(pos, out, -np.inf)
 
 
 def normal_logpdf(x, mu, sd):
@@ -200,19 +205,31 @@ class HDDM:
                       "sz": 0.01 if "sz" in self.include else 0.0,
                       "st": 0.001 if "st" in self.include else 0.0}
 
+    _COL = {"v": 0, "sv": 1, "a": 2, "sz": 4, "t": 5, "st": 6}
+
     def node_table(self, over=None):
-        """(n_nodes, 8) parameter table v, sv, a, z, sz, t, st, p_outlier."""
-        over = over or {}
-        P = np.empty((self.n_nodes, 8))
-        sub = {f: over.get(f, self.subj[f]) for f in self.FAMILIES}
-        P[:, 0] = sub["v"][self.node_unit["v"]]
-        P[:, 1] = over.get("sv", self.inter["sv"])
-        P[:, 2] = sub["a"][self.node_unit["a"]]
-        P[:, 3] = 0.5
-        P[:, 4] = over.get("sz", self.inter["sz"])
-        P[:, 5] = sub["t"][self.node_unit["t"]]
-        P[:, 6] = over.get("st", self.inter["st"])
-        P[:, 7] = self.p_outlier
+        """(n_nodes, 8) parameter table v, sv, a, z, sz, t, st, p_outlier. The
+        table at the current values is kept and only the columns in `over`
+        (the one parameter a slice step moves) are rewritten."""
+        key = (self.subj["v"].tobytes(), self.subj["a"].tobytes(), self.subj["t"].tobytes(),
+               self.inter["sv"], self.inter["sz"], self.inter["st"])
+        if getattr(self, "_table_key", None) != key:
+            P = np.empty((self.n_nodes, 8))
+            P[:, 0] = self.subj["v"][self.node_unit["v"]]
+            P[:, 1] = self.inter["sv"]
+            P[:, 2] = self.subj["a"][self.node_unit["a"]]
+            P[:, 3] = 0.5
+            P[:, 4] = self.inter["sz"]
+            P[:, 5] = self.subj["t"][self.node_unit["t"]]
+            P[:, 6] = self.inter["st"]
+            P[:, 7] = self.p_outlier
+            self._table, self._table_key = P, key
+        if not over:
+            return self._table
+        P = self._table.copy()
+        for name, val in over.items():
+            col = self._COL[name]
+            P[:, col] = val[self.node_unit[name]] if name in self.FAMILIES else val
         return P
 
     def node_logp(self, over=None):
