@@ -44,19 +44,14 @@ WIENER_PARAMS = {"err": 1e-4, "n_st": 2, "n_sz": 2, "use_adaptive": 1, "simps_er
 
 # ---------------------------------------------------------------- log densities
 
-_TINY = np.finfo(np.float64).tiny
-
-
 def gamma_logpdf_mean_sd(x, mean, sd):
     """pm.Gamma(alpha=mean^2/sd^2, beta=mean/sd^2) (base.py:642-667)."""
     x = np.asarray(x, dtype=np.float64)
     shape = mean ** 2 / sd ** 2
     rate = mean / sd ** 2
-    pos = x > 0
-    # log of a clamped copy: no floating-point warnings to silence per call
-    out = shape * np.log(rate) - special.gammaln(shape) + (shape - 1) * np.log(
-        np.where(pos, x, _TINY)) - rate * x
-    return np.where(pos, out, -np.inf)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        out = shape * np.log(rate) - special.gammaln(shape) + (shape - 1) * np.log(x) - rate * x
+    return np.where(x > 0, out, -np.inf)
 
 
 def normal_logpdf(x, mu, sd):
