@@ -141,15 +141,172 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
   }
 }
 
+// Tail of the resident-data wiener_like (TAIL fast kernels): the call's
+// reduction and publication done by the fast kernel itself, so a call whose
+// trials all finish at level 0 is ONE kernel. Three levels, each "last to
+// arrive sums, in a fixed order":
+//   block: each wave leaves its partial in LDS and takes an LDS ticket; the
+//          last wave of the block sums the block's waves -> bpart[block];
+//   group: that wave takes the ticket of its group of 64 blocks; the last
+//          block of a group sums the group's 64 block partials -> gpart[g];
+//   top:   the last group sums the group partials (lane-strided) and, if no
+//          trial was deferred, writes {sum, #zeros, status} and then the
+//          completion word `seq` into the mapped result slot. Otherwise it
+//          writes seq | kDeferWord and the host runs slow_kernel +
+//          finalize_kernel (which fold the per-wave partials A.out[wave]).
+// Tickets and the deferred counter are reset by their last reader, so they are
+// zero at rest.
+//
+// Cross-XCD visibility without L2 write-backs: an agent-scope release fence
+// (__threadfence) flushes the XCD's whole L2 (buffer_wbl2); one per wave
+// measured +0.21 ms per 1M trials. Here the data handed between blocks is
+// stored and loaded with agent-scope relaxed atomics, which are coherent
+// across XCDs by themselves; the arriving wave waits for its stores to
+// complete (s_waitcnt 0) before it takes its ticket, and a reader issues its
+// loads only after its ticket said it was last. Only one wave per block pays
+// that round trip (one per wave measured +23 us per 1M trials).
+struct Tail {
+  unsigned* grp;       // per-group arrival tickets (ceil(nblocks / 64))
+  unsigned* top;       // [0] group ticket, [1] deferred-trial count
+  double* bpart;       // per-block partial sums
+  int* bzero;          // per-block zero counts
+  double* gpart;       // per-group partial sums
+  int* gzero;          // per-group zero counts
+  double* out;         // mapped result slot {sum, zeros, status, word}
+  int* status;
+  unsigned long long seq;
+};
+
+template <class T>
+__device__ inline void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ inline T ld_agent(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// this wave's earlier stores have completed (vmcnt = expcnt = lgkmcnt = 0);
+// the signal fences keep the compiler from moving memory operations across it
+__device__ inline void stores_done() {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_s_waitcnt(0);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ inline unsigned ticket(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+struct TailLds {
+  double part[kBlock / 64];
+  int zero[kBlock / 64];
+  unsigned nslow;
+  unsigned cnt;
+};
+
+template <bool TAIL>
+__device__ inline void fast_tail(const TrialArgs& A, const Tail& T, TailLds& L, double lp, int zs,
+                                 int lane, int nslow) {
+  if (!TAIL) return;
+  constexpr int WPB = kBlock / 64;
+  const int w = threadIdx.x >> 6;
+  unsigned t = 0;
+  if (lane == 0) {
+    L.part[w] = lp;
+    L.zero[w] = zs;
+    if (nslow) atomicAdd(&L.nslow, (unsigned)nslow);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    t = atomicAdd(&L.cnt, 1u);
+  }
+  t = __shfl(t, 0, 64);
+  if (t != (unsigned)(WPB - 1)) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const int64_t blk = blockIdx.x;
+  const int64_t nblk = gridDim.x;
+  const int64_t g = blk >> 6;
+  const int64_t ng = (nblk + 63) >> 6;
+  const int gsz = (int)((nblk - (g << 6)) < 64 ? (nblk - (g << 6)) : 64);
+  if (lane == 0) {
+    double s = 0.0;
+    int z = 0;
+    for (int k = 0; k < WPB; ++k) {
+      s += L.part[k];
+      z += L.zero[k];
+    }
+    st_agent(&T.bpart[blk], s);
+    st_agent(&T.bzero[blk], z);
+    if (L.nslow) ticket(&T.top[1], L.nslow);
+    stores_done();
+    t = ticket(&T.grp[g], 1u);
+  }
+  t = __shfl(t, 0, 64);
+  if (t != (unsigned)(gsz - 1)) return;
+  double s = 0.0;
+  int z = 0;
+  if (lane < gsz) {
+    s = ld_agent(&T.bpart[(g << 6) + lane]);
+    z = ld_agent(&T.bzero[(g << 6) + lane]);
+  }
+  s = wave_sum(s);
+  for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
+  unsigned t2 = 0;
+  if (lane == 0) {
+    st_agent(&T.gpart[g], s);
+    st_agent(&T.gzero[g], z);
+    st_agent(&T.grp[g], 0u);
+    stores_done();
+    t2 = ticket(&T.top[0], 1u);
+  }
+  t2 = __shfl(t2, 0, 64);
+  if (t2 != (unsigned)(ng - 1)) return;
+  double s0 = 0.0, s1 = 0.0;
+  long long zz = 0;
+  int64_t j = lane;
+  for (; j + 64 < ng; j += 128) {
+    s0 += ld_agent(&T.gpart[j]);
+    s1 += ld_agent(&T.gpart[j + 64]);
+    zz += (long long)ld_agent(&T.gzero[j]) + ld_agent(&T.gzero[j + 64]);
+  }
+  if (j < ng) {
+    s0 += ld_agent(&T.gpart[j]);
+    zz += ld_agent(&T.gzero[j]);
+  }
+  s = wave_sum(s0 + s1);
+  zz = wave_sum_ll(zz);
+  if (lane == 0) {
+    const unsigned deferred = __hip_atomic_exchange(&T.top[1], 0u, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    st_agent(&T.top[0], 0u);
+    unsigned long long word = T.seq;
+    if (deferred == 0) {
+      T.out[0] = s;
+      T.out[1] = (double)zz;
+      T.out[2] = (double)atomicExch(T.status, 0);
+    } else {
+      word |= kDeferWord;
+    }
+    __threadfence_system();
+    reinterpret_cast<volatile unsigned long long*>(T.out)[3] = word;
+    __threadfence_system();
+  }
+}
+
 // Level-0 fast pass (MODE in kDirect..kAdaptTZ). Trials whose root Simpson
 // tests all pass are finished here; the others are compacted per WAVE into
 // `wl` (lane ids, one byte each, 64 slots per wave) and counted in
 // `wl_n[wave]` for slow_kernel. Barrier-free: every wave writes its own
 // partial sum / zero count (A.out[wave], A.zeros[wave]) and worklist, so a
-// wave that finishes early never waits for its block.
-template <int MODE, bool COUNT, int OUT>
+// wave that finishes early never waits for its block (TAIL: see fast_tail).
+template <int MODE, bool COUNT, int OUT, bool TAIL>
 __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
+void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
+  __shared__ TailLds L;
+  if (TAIL) {
+    if (threadIdx.x == 0) {
+      L.nslow = 0u;
+      L.cnt = 0u;
+    }
+    __syncthreads();
+  }
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int64_t wave = i >> 6;
   const int lane = threadIdx.x & 63;
@@ -173,14 +330,17 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
       }
     }
   }
+  int nslow = 0;
   if (MODE != kDirect) {
     const unsigned long long b = __ballot(slow);
     if (slow) wl[wave * 64 + __popcll(b & ((1ull << lane) - 1ull))] = (unsigned char)lane;
-    if (lane == 0) wl_n[wave] = __popcll(b);
+    nslow = __popcll(b);
+    if (lane == 0) wl_n[wave] = nslow;
   }
+  int zs = 0;
   if (OUT == OUT_SUM || COUNT) {
     lp = wave_sum(lp);
-    const int zs = __popcll(__ballot(zero != 0));
+    zs = __popcll(__ballot(zero != 0));
     if (COUNT) ne = wave_sum_ll(ne);
     if (lane == 0) {
       if (OUT == OUT_SUM) {
@@ -190,6 +350,7 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
       if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
     }
   }
+  if (OUT == OUT_SUM && !COUNT) fast_tail<TAIL>(A, T, L, lp, zs, lane, nslow);
 }
 
 // General pass over the trials the fast pass deferred. The fast pass leaves
@@ -566,14 +727,21 @@ static void launch_generic(const TrialArgs& A, int64_t nb, hipStream_t s) {
 }
 
 // fast pass + (for adaptive modes) the slow pass on the deferred trials
+template <int MODE, int STK, bool COUNT, int OUT>
+static void launch_slow(const TrialArgs& A, int64_t nb, const unsigned char* wl, const int* wl_n,
+                        hipStream_t s) {
+  hipLaunchKernelGGL((slow_kernel<MODE, STK, COUNT, OUT>), dim3(slow_grid(nb)), dim3(64), 0, s, A,
+                     wl, wl_n, nb, nb);
+}
+
 template <int MODE, bool COUNT, int OUT>
 static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned char* wl,
                             int* wl_n, hipStream_t s, hipEvent_t fast_done) {
   // both fast kernels leave one partial / worklist per 64 trials
   constexpr int TPB = 64;
   const int64_t nb = (n + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
-                     A, wl, wl_n);
+  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT, false>), dim3(blocks_for(n)), dim3(kBlock), 0,
+                     s, A, wl, wl_n, Tail{});
   if (fast_done) (void)hipEventRecord(fast_done, s);
   if (MODE == kDirect) return;
   const int64_t g = slow_grid(nb);
@@ -661,6 +829,64 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
   if (nb == 0) return;
   if (evals) launch_count<true>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s, fast_done);
   else launch_count<false>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s, fast_done);
+}
+
+static TrialArgs sum_args(const double* x, int64_t n, const Params& P, const Knobs& K,
+                          double* part, int* zeros, int* status) {
+  TrialArgs A;
+  A.x = x;
+  A.n = n;
+  A.P = P;
+  A.K = K;
+  A.wp_outlier = K.w_outlier * P.p_outlier;
+  A.out = part;
+  A.zeros = zeros;
+  A.evals = nullptr;
+  A.status = status;
+  A.logp = 0;
+  return A;
+}
+
+int64_t tail_blocks(int64_t n) { return blocks_for(n); }
+int64_t tail_groups(int64_t n) { return (blocks_for(n) + 63) / 64; }
+
+bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                     int* zeros, int* status, unsigned char* wl, int* wl_n, unsigned* grp,
+                     unsigned* top, double* bpart, int* bzero, double* gpart, int* gzero,
+                     double* out, unsigned long long seq, hipStream_t s) {
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  if (n <= 0 || mode > kAdaptTZ) return false;
+  const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
+  const Tail T{grp, top, bpart, bzero, gpart, gzero, out, status, seq};
+  const dim3 g(blocks_for(n)), b(kBlock);
+  switch (mode) {
+    case kDirect: hipLaunchKernelGGL((fast_kernel<kDirect, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
+    case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
+    case kAdaptZ: hipLaunchKernelGGL((fast_kernel<kAdaptZ, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
+    default: hipLaunchKernelGGL((fast_kernel<kAdaptTZ, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
+  }
+  return true;
+}
+
+void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s) {
+  const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
+  const int64_t nb = (n + 63) / 64;
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  const int stk = stack_kind(K);
+#define SLOW(M_)                                                        \
+  do {                                                                  \
+    if (stk == 0) launch_slow<M_, 0, false, OUT_SUM>(A, nb, wl, wl_n, s); \
+    else if (stk == 1) launch_slow<M_, 1, false, OUT_SUM>(A, nb, wl, wl_n, s); \
+    else launch_slow<M_, 2, false, OUT_SUM>(A, nb, wl, wl_n, s);        \
+  } while (0)
+  switch (mode) {
+    case kAdaptT: SLOW(kAdaptT); break;
+    case kAdaptZ: SLOW(kAdaptZ); break;
+    case kAdaptTZ: SLOW(kAdaptTZ); break;
+    default: break;  // kDirect never defers
+  }
+#undef SLOW
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,

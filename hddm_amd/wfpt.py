@@ -141,9 +141,9 @@ class Dataset:
     parameters change per proposal). Optional `node_id` groups trials into
     `n_nodes` likelihood nodes scored together by `wiener_like_nodes`."""
 
-    def __init__(self, rt, node_id=None, n_nodes=None, device=None):
+    def __init__(self, rt, node_id=None, n_nodes=None, device=None, ctx=None):
         rt = np.ascontiguousarray(np.asarray(rt, dtype=np.float64).ravel())
-        self.ctx = _lib.context(device)
+        self.ctx = ctx if ctx is not None else _lib.context(device)
         self.n = rt.shape[0]
         h = _lib._VP()
         if node_id is not None:
