@@ -38,8 +38,7 @@ struct FastWaves {
 // 2-wave budget (1 wave / SIMD); 2 keeps them at 256 with a little more scratch.
 #ifndef WFPT_SLOW_WAVES
 #define WFPT_SLOW_WAVES 2
-#endif
-// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
+#endif// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
 // occupy (256 CUs x 4 SIMDs x WFPT_SLOW_WAVES).
 #ifndef WFPT_SLOW_GRID
 #define WFPT_SLOW_GRID 2048
@@ -296,27 +295,24 @@ __device__ inline void fast_tail(const TrialArgs& A, const Tail& T, TailLds& L, 
 // `wl_n[wave]` for slow_kernel. Barrier-free: every wave writes its own
 // partial sum / zero count (A.out[wave], A.zeros[wave]) and worklist, so a
 // wave that finishes early never waits for its block (TAIL: see fast_tail).
-template <int MODE, bool COUNT, int OUT, bool TAIL>
-__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
-  __shared__ TailLds L;
-  if (TAIL) {
-    if (threadIdx.x == 0) {
-      L.nslow = 0u;
-      L.cnt = 0u;
-    }
-    __syncthreads();
-  }
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const int64_t wave = i >> 6;
-  const int lane = threadIdx.x & 63;
+//
+// fast_chunk: one 64-trial chunk of the level-0 pass for the calling wave: trial
+// i = c*64 + lane with RT xi (ignored when i >= n). Writes the chunk's
+// worklist, partial sum and zero count; returns the wave-reduced partial (lp,
+// zs) and the deferred count for the fused tail.
+template <int MODE, bool COUNT, int OUT>
+__device__ __forceinline__ void fast_chunk(const TrialArgs& A, unsigned char* wl, int* wl_n,
+                                           int64_t c, int lane, double xi, double& lp_out,
+                                           int& zs_out, int& nslow_out) {
+  const int64_t i = c * 64 + lane;
+  const int64_t wave = c;
   long long ne = 0;
   double lp = 0.0;
   int zero = 0;
   bool slow = false;
   if (i < A.n) {
     int valid = 0;
-    double p = fast_pdf<MODE>(A.x[i], A.P, A.K, slow, valid);
+    double p = fast_pdf<MODE>(xi, A.P, A.K, slow, valid);
     if (!slow) {
       if (COUNT && valid) ne = fast_evals(MODE);
       if (OUT == OUT_ARRAY) {
@@ -350,6 +346,27 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
       if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
     }
   }
+  lp_out = lp;
+  zs_out = zs;
+  nslow_out = nslow;
+}
+
+template <int MODE, bool COUNT, int OUT, bool TAIL>
+__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
+  __shared__ TailLds L;
+  if (TAIL) {
+    if (threadIdx.x == 0) {
+      L.nslow = 0u;
+      L.cnt = 0u;
+    }
+    __syncthreads();
+  }
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  double lp;
+  int zs, nslow;
+  fast_chunk<MODE, COUNT, OUT>(A, wl, wl_n, i >> 6, lane, i < A.n ? A.x[i] : 0.0, lp, zs, nslow);
   if (OUT == OUT_SUM && !COUNT) fast_tail<TAIL>(A, T, L, lp, zs, lane, nslow);
 }
 
