@@ -32,8 +32,9 @@ def _stale(target, deps):
 
 
 def build(force=False, verbose=False, defines=(), out=None):
-    """Compile libwfpt_amd.so. `defines` (e.g. ["WFPT_FAST_WAVES=3"]) and `out`
-    build experiment variants next to the default library."""
+    """Compile libwfpt_amd.so. `defines` (e.g. ["WFPT_FAST_WAVES=3"]; entries
+    starting with '-' are extra compiler flags) and `out` build experiment
+    variants next to the default library."""
     os.makedirs(LIBDIR, exist_ok=True)
     lib = out or LIB
     deps = [os.path.join(CSRC, f) for f in DEPS] + [os.path.join(ROOT, "include", "wfpt_amd.h")]
@@ -43,8 +44,9 @@ def build(force=False, verbose=False, defines=(), out=None):
     tag = os.path.splitext(os.path.basename(lib))[0]
     for src in SOURCES:
         obj = os.path.join(LIBDIR, tag + "_" + os.path.splitext(src)[0] + ".o")
-        cmd = [HIPCC, *CFLAGS, *[f"-D{d}" for d in defines], "-c", os.path.join(CSRC, src),
-               "-o", obj]
+        flags = [f for d in defines if d.startswith("-") for f in d.split()]
+        cmd = [HIPCC, *CFLAGS, *flags, *[f"-D{d}" for d in defines if not d.startswith("-")],
+               "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
