@@ -79,15 +79,16 @@ def load_traffic(n_trials):
     the committed rocprofv3 PMC summary (profiles/traffic.json), if present."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
-        return None, None
+        return None, None, None
     try:
         with open(path) as fh:
             t = json.load(fh)
         if int(t.get("n_trials", -1)) == int(n_trials):
-            return float(t["hbm_bytes_per_launch"]), t.get("valu_issue_utilisation")
+            return (float(t["hbm_bytes_per_launch"]), t.get("valu_issue_utilisation"),
+                    t.get("fp64_lane_ops_per_trial"))
     except Exception:
-        return None, None
-    return None, None
+        return None, None, None
+    return None, None, None
 
 
 def main():
@@ -169,7 +170,10 @@ def main():
     w_trial = evals_per_trial * W_EVAL + W_EPI
     k_avg_s = (k_ms / 1e3) / max(launches, 1)
     achieved = n * w_trial / k_avg_s / 1e12
-    traffic, valu_util = load_traffic(n)
+    traffic, valu_util, f64_per_trial = load_traffic(n)
+    # hardware view: fp64 VALU lane-ops the kernel actually executes per trial
+    # (rocprofv3 SQ_INSTS_VALU_*_F64 x 64, profiles/traffic.json) over its time
+    exec_tops = n * f64_per_trial / k_avg_s / 1e12 if f64_per_trial else None
     out = {
         "metric": METRIC,
         "value": value,
@@ -199,7 +203,11 @@ def main():
                      "w_trial_lane_ops": w_trial,
                      # hardware view (rocprofv3 PMC, profiles/traffic.json): share of SIMD
                      # cycles issuing VALU (4 cycles per wave64 fp64 op, 2 otherwise)
-                     "valu_issue_utilisation": valu_util},
+                     "valu_issue_utilisation": valu_util,
+                     # frac above is algorithmic (the reference's op count, SURVEY.md
+                     # 8d); this is executed fp64 work over the same peak
+                     "executed_fp64": exec_tops,
+                     "executed_frac": exec_tops / (PEAK_LANE_OPS / 1e12) if exec_tops else None},
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(x, a.cpu_seconds)
