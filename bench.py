@@ -146,8 +146,11 @@ def main():
     for _ in range(a.steps):
         val = step()
     ctx.synchronize()
-    barrier()
+    # each rank's clock stops when its own K calls are done (every call ends in
+    # the all-reduce, so ranks finish together); the closing barrier aligns the
+    # ranks for the next phase and the max over ranks below is the job time
     el = time.perf_counter() - t0
+    barrier()
     # the same K calls again with HIP events recorded on the library's stream
     # around the likelihood kernels of every call: per-launch kernel time
     ctx.profile(ctx.PROF_EVENTS)
