@@ -38,8 +38,7 @@ struct FastWaves {
 // 2-wave budget (1 wave / SIMD); 2 keeps them at 256 with a little more scratch.
 #ifndef WFPT_SLOW_WAVES
 #define WFPT_SLOW_WAVES 2
-#endif
-// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
+#endif// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
 // occupy (256 CUs x 4 SIMDs x WFPT_SLOW_WAVES).
 #ifndef WFPT_SLOW_GRID
 #define WFPT_SLOW_GRID 2048
@@ -362,6 +361,8 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
     }
     __syncthreads();
   }
+  // ascending |rt| in dispatch order: the costlier short-RT chunks start first
+  // (dispatching largest |rt| first measured 3% slower)
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   double lp;
