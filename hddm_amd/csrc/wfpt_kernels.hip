@@ -17,6 +17,13 @@
 namespace wfpt {
 
 constexpr int kBlock = 256;
+// Threads per block of the level-0 fast kernel (barrier-free, one chunk of 64
+// trials per wave): the block is only the hardware's dispatch unit.
+#ifndef WFPT_FAST_BLOCK
+#define WFPT_FAST_BLOCK 256
+#endif
+constexpr int kFastBlock = WFPT_FAST_BLOCK;
+static inline int64_t fast_blocks(int64_t n) { return (n + kFastBlock - 1) / kFastBlock; }
 
 // Minimum waves per SIMD requested for the level-0 fast kernels (0 = let the
 // compiler choose): WFPT_FAST_WAVES for the 1-D / direct modes,
@@ -38,11 +45,13 @@ struct FastWaves {
 // 2-wave budget (1 wave / SIMD); 2 keeps them at 256 with a little more scratch.
 #ifndef WFPT_SLOW_WAVES
 #define WFPT_SLOW_WAVES 2
-#endif// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
+#endif
+// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
 // occupy (256 CUs x 4 SIMDs x WFPT_SLOW_WAVES).
 #ifndef WFPT_SLOW_GRID
 #define WFPT_SLOW_GRID 2048
 #endif
+
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
 
 __device__ inline double wave_sum(double v) {
@@ -195,8 +204,8 @@ __device__ inline unsigned ticket(unsigned* p, unsigned v) {
 }
 
 struct TailLds {
-  double part[kBlock / 64];
-  int zero[kBlock / 64];
+  double part[kFastBlock / 64];
+  int zero[kFastBlock / 64];
   unsigned nslow;
   unsigned cnt;
 };
@@ -205,7 +214,7 @@ template <bool TAIL>
 __device__ inline void fast_tail(const TrialArgs& A, const Tail& T, TailLds& L, double lp, int zs,
                                  int lane, int nslow) {
   if (!TAIL) return;
-  constexpr int WPB = kBlock / 64;
+  constexpr int WPB = kFastBlock / 64;
   const int w = threadIdx.x >> 6;
   unsigned t = 0;
   if (lane == 0) {
@@ -351,7 +360,7 @@ __device__ __forceinline__ void fast_chunk(const TrialArgs& A, unsigned char* wl
 }
 
 template <int MODE, bool COUNT, int OUT, bool TAIL>
-__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
   __shared__ TailLds L;
   if (TAIL) {
@@ -363,7 +372,7 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
   }
   // ascending |rt| in dispatch order: the costlier short-RT chunks start first
   // (dispatching largest |rt| first measured 3% slower)
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   double lp;
   int zs, nslow;
@@ -761,7 +770,7 @@ static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned cha
   // both fast kernels leave one partial / worklist per 64 trials
   constexpr int TPB = 64;
   const int64_t nb = (n + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT, false>), dim3(blocks_for(n)), dim3(kBlock), 0,
+  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT, false>), dim3(fast_blocks(n)), dim3(kFastBlock), 0,
                      s, A, wl, wl_n, Tail{});
   if (fast_done) (void)hipEventRecord(fast_done, s);
   if (MODE == kDirect) return;
@@ -868,8 +877,8 @@ static TrialArgs sum_args(const double* x, int64_t n, const Params& P, const Kno
   return A;
 }
 
-int64_t tail_blocks(int64_t n) { return blocks_for(n); }
-int64_t tail_groups(int64_t n) { return (blocks_for(n) + 63) / 64; }
+int64_t tail_blocks(int64_t n) { return fast_blocks(n); }
+int64_t tail_groups(int64_t n) { return (fast_blocks(n) + 63) / 64; }
 
 bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                      int* zeros, int* status, unsigned char* wl, int* wl_n, unsigned* grp,
@@ -879,7 +888,7 @@ bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K
   if (n <= 0 || mode > kAdaptTZ) return false;
   const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
   const Tail T{grp, top, bpart, bzero, gpart, gzero, out, status, seq};
-  const dim3 g(blocks_for(n)), b(kBlock);
+  const dim3 g(fast_blocks(n)), b(kFastBlock);
   switch (mode) {
     case kDirect: hipLaunchKernelGGL((fast_kernel<kDirect, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
     case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
