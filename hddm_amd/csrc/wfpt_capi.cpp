@@ -125,6 +125,7 @@ struct wfpt_ctx {
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
   bool tail = false;           // WFPT_TAIL=1: one-kernel resident wiener_like (run_sum_tail)
+  bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
   double k_ms = 0.0;
@@ -147,6 +148,9 @@ struct wfpt_ds {
   // (MCMC proposals move the parameters little: deferral persists), then the
   // one-kernel path is tried again
   mutable int defers = 0;
+  // the last call on this dataset deferred no trial: the next one runs the
+  // level-0 pass + finalize only (run_sum_fast), no slow pass
+  mutable bool no_defer = false;
 };
 
 namespace {
@@ -234,7 +238,7 @@ int check_status_value(double st) {
 // Fast pass (+ slow pass) + finalize over device x[n]; the 3-double result
 // {sum, zeros, status} lands in `out` (mapped host memory or device).
 int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
-            const wfpt::Knobs& K, double* out) {
+            const wfpt::Knobs& K, double* out, int keep = -1) {
   const int64_t nb = wfpt::partials_for(n, P, K);
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
@@ -250,7 +254,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   int64_t off = 0, cnt = 0;
   wfpt::final_partials(n, P, K, &off, &cnt);
   wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, out, ++c->seq,
-                        c->stream);
+                        c->stream, keep);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -307,13 +311,21 @@ int wait_result(wfpt_ctx* c, const double* r) {
   return WFPT_OK;
 }
 
-// Waits for the call and decodes {sum, zeros, status} from host memory `r`.
-int read_sum(wfpt_ctx* c, const double* r, double* out) {
-  if (int rc = wait_result(c, r)) return rc;
-  if (int rc = check_status_value(r[2])) return rc;
+// Decodes {sum, zeros, status} from host memory `r` of a finished call;
+// *deferred (if given) = the level-0 pass deferred trials.
+int decode_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr) {
+  const int st = (int)r[2];
+  if (deferred) *deferred = (st & wfpt::kStatusDeferred) != 0;
+  if (int rc = check_status_value((double)(st & ~wfpt::kStatusDeferred))) return rc;
   if (int rc = finish_profile(c)) return rc;
   *out = (r[1] > 0) ? -INFINITY : r[0];
   return WFPT_OK;
+}
+
+// Waits for the call and decodes its result.
+int read_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr) {
+  if (int rc = wait_result(c, r)) return rc;
+  return decode_sum(c, r, out, deferred);
 }
 
 // Resident-data sum as ONE kernel (fast_kernel<..., TAIL>; WFPT_TAIL=1): the
@@ -372,6 +384,43 @@ int run_sum_tail(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
   return read_sum(c, c->mres, out);
 }
 
+// Resident-data sum predicted to defer nothing (the dataset's last call did
+// not): level-0 pass + finalize over its per-64-trial partials, no slow pass
+// (-4.6 us of empty slow kernel per call). If the level-0 pass did defer
+// trials this time (kStatusDeferred in the result), the slow pass and a second
+// finalize run over the intact partials and worklists, so the result is always
+// the full one; only that call pays a host round trip. Returns -1 when the
+// path does not apply (nothing launched).
+int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
+                 double* out) {
+  const int64_t n = d->n;
+  if (c->count || !d->no_defer || n <= 0) return -1;
+  const int64_t nb = wfpt::partials_for(n, P, K);
+  HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
+  HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
+  if (int rc = reserve_worklist(c, n)) return rc;
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  if (!wfpt::launch_fast_pass(d->x, n, P, K, c->part.p, c->zero.p, c->status, c->wl.p, c->wl_n.p,
+                              c->stream, c->profile ? c->ev1 : nullptr))
+    return -1;
+  HIP_TRY(hipGetLastError());
+  const int64_t nw = (n + 63) / 64;
+  wfpt::launch_finalize(c->part.p, c->zero.p, nw, c->status, c->mres_dev, ++c->seq, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (int rc = wait_result(c, c->mres)) return rc;
+  if (((int)c->mres[2] & wfpt::kStatusDeferred) == 0) return decode_sum(c, c->mres, out);
+  d->no_defer = false;
+  wfpt::launch_slow_pass(d->x, n, P, K, c->part.p, c->zero.p, c->status, c->wl.p, c->wl_n.p,
+                         c->stream);
+  HIP_TRY(hipGetLastError());
+  int64_t off = 0, cnt = 0;
+  wfpt::final_partials(n, P, K, &off, &cnt);
+  wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, c->mres_dev, ++c->seq,
+                        c->stream);
+  HIP_TRY(hipGetLastError());
+  return read_sum(c, c->mres, out);
+}
+
 int upload(wfpt_ctx* c, const double* x, int64_t n) {
   HIP_TRY(c->x.reserve(std::max<int64_t>(n, 1)));
   if (n > 0)
@@ -405,6 +454,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* tm = std::getenv("WFPT_TAIL")) c->tail = std::strcmp(tm, "1") == 0;
+  if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -552,10 +602,15 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  const int rc = run_sum_tail(c, d, P, K, out);
+  int rc = run_sum_tail(c, d, P, K, out);
+  if (rc >= 0) return rc;
+  rc = run_sum_fast(c, d, P, K, out);
   if (rc >= 0) return rc;
   if (int rc2 = run_sum(c, d->x, d->n, P, K, c->mres_dev)) return rc2;
-  return read_sum(c, c->mres, out);
+  bool deferred = true;
+  rc = read_sum(c, c->mres, out, &deferred);
+  if (rc == WFPT_OK && c->fast_only) d->no_defer = !deferred;
+  return rc;
 }
 
 int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
@@ -779,7 +834,8 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   HIP_TRY(c->res.reserve(3));
-  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p)) return rc;
+  // the deferred-trials bit is per rank: keep it out of the summed status
+  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p, ~wfpt::kStatusDeferred)) return rc;
   // {sum, zeros, status} of every rank summed: any zero trial or failure anywhere
   // reaches every rank
   NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 3, ncclDouble, ncclSum, c->comm, c->stream));

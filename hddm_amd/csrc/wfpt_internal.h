@@ -39,12 +39,21 @@ bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K
                      double* out, unsigned long long seq, hipStream_t s);
 void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                       int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s);
+// Status bit the level-0 pass of a sum sets when it deferred trials (besides
+// the error bits 1 = Simpson depth, 2 = evaluation budget).
+constexpr int kStatusDeferred = 4;
+// The level-0 pass alone (adaptive modes; false, nothing launched, otherwise):
+// per-64-trial partials in part[0, ceil(n/64)) + worklists, and
+// kStatusDeferred in *status if any trial still needs the slow pass.
+bool launch_fast_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s,
+                      hipEvent_t fast_done);
 // res[0..2] (device) -> out[0..2] (mapped host), then out[3] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
-// out[0..2] = {sum, #zero trials, status flags}, then out[3] = seq (as a
-// 64-bit word) once they are visible; resets *status to 0.
+// out[0..2] = {sum, #zero trials, status flags & keep}, then out[3] = seq (as
+// a 64-bit word) once they are visible; resets *status to 0.
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
-                     unsigned long long seq, hipStream_t s);
+                     unsigned long long seq, hipStream_t s, int keep = -1);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
 // two-pass fast path; d_idx / d_par hold up to n deferred trials, *n_defer
 // must be 0 on the stream), or -1 (mixed / fixed

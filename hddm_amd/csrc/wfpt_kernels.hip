@@ -340,6 +340,9 @@ __device__ __forceinline__ void fast_chunk(const TrialArgs& A, unsigned char* wl
     if (slow) wl[wave * 64 + __popcll(b & ((1ull << lane) - 1ull))] = (unsigned char)lane;
     nslow = __popcll(b);
     if (lane == 0) wl_n[wave] = nslow;
+    // tells the host this call deferred trials (the fast-only call sequence
+    // of wfpt_capi.cpp relies on it)
+    if (OUT == OUT_SUM && lane == 0 && nslow) atomicOr(A.status, kStatusDeferred);
   }
   int zs = 0;
   if (OUT == OUT_SUM || COUNT) {
@@ -467,7 +470,7 @@ __host__ __device__ inline int64_t slow_grid(int64_t nl) { return nl < kSlowGrid
 // in flight).
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
                                                         int64_t nb, int* status, double* out,
-                                                        unsigned long long seq) {
+                                                        unsigned long long seq, int keep) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
@@ -504,7 +507,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     *status = 0;
     out[0] = t;
     out[1] = (double)zz;
-    out[2] = (double)st;
+    out[2] = (double)(st & keep);
     __threadfence_system();
     // completion word, written after the results are visible: the host may
     // poll it instead of waiting on the stream
@@ -898,6 +901,22 @@ bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K
   return true;
 }
 
+bool launch_fast_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s,
+                      hipEvent_t fast_done) {
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  if (n <= 0 || mode < kAdaptT || mode > kAdaptTZ) return false;
+  const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
+  const dim3 g(fast_blocks(n)), b(kFastBlock);
+  switch (mode) {
+    case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM, false>), g, b, 0, s, A, wl, wl_n, Tail{}); break;
+    case kAdaptZ: hipLaunchKernelGGL((fast_kernel<kAdaptZ, false, OUT_SUM, false>), g, b, 0, s, A, wl, wl_n, Tail{}); break;
+    default: hipLaunchKernelGGL((fast_kernel<kAdaptTZ, false, OUT_SUM, false>), g, b, 0, s, A, wl, wl_n, Tail{}); break;
+  }
+  if (fast_done) (void)hipEventRecord(fast_done, s);
+  return true;
+}
+
 void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                       int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s) {
   const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
@@ -920,9 +939,9 @@ void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& 
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
-                     unsigned long long seq, hipStream_t s) {
+                     unsigned long long seq, hipStream_t s, int keep) {
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, status, out,
-                     seq);
+                     seq, keep);
 }
 
 template <int MODE, bool COUNT>

@@ -397,3 +397,34 @@ def test_resident_one_kernel_tail(gpu, oracle_lib, tail_ctx):
     with pytest.raises(NotImplementedError):
         dso.wiener_like(0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-10, n_st=40, n_sz=40, simps_err=0.0)
     assert np.isfinite(dso.wiener_like(0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-8))
+
+
+def test_resident_fast_only_prediction(gpu, oracle_lib):
+    """A resident dataset whose last call deferred no trial runs the level-0 pass
+    + finalize only (run_sum_fast in wfpt_capi.cpp); when that prediction is
+    wrong the slow pass runs after all. Alternating deferring / non-deferring
+    parameters on one dataset exercises both transitions; every result must
+    equal the host-array path (always the full sequence) and the oracle."""
+    rng = np.random.default_rng(20261018)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    pinned = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    stress = (-2.5, 2.2, 0.6, 0.45, 0.35, 0.25, 0.3)
+    st_only = (0.8, 0.0, 1.6, 0.45, 0.0, 0.25, 0.2)
+    sz_only = (0.8, 0.0, 1.6, 0.45, 0.3, 0.25, 0.0)
+    for n in (65, 20_000, 300_001):
+        x = rng.choice([-1.0, 1.0], n) * (0.3 + rng.gamma(2.0, 0.45, n))
+        ds = gpu.Dataset(x)
+        seq = [pinned, pinned, stress, stress, pinned, pinned, st_only, sz_only, stress, pinned]
+        for args in seq:
+            got = ds.wiener_like(*args, *kn)
+            host = gpu.wiener_like(x, *args, *kn)
+            assert abs(got - host) <= 1e-11 * max(abs(host), 1.0), (n, args, got, host)
+            if n <= 20_000:
+                ref = oracle_lib.pdf_array(x, *args, kn[0], 1, *kn[1:5], kn[5], kn[6])
+                assert_total(got, ref, f"fast-only n={n} {args}")
+    # a Simpson-stack overflow in a mispredicted call still fails loudly
+    ds = gpu.Dataset(np.array([0.35, 0.9, -1.3]))
+    assert np.isfinite(ds.wiener_like(0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-8, n_st=2, n_sz=2,
+                                      simps_err=1.0))
+    with pytest.raises(NotImplementedError):
+        ds.wiener_like(0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-10, n_st=40, n_sz=40, simps_err=0.0)
