@@ -1,23 +1,30 @@
 #!/usr/bin/env python3
 """Headline benchmark: full-DDM trial-likelihood evaluations / s on MI355X.
 
-Workload (BASELINE.json configs[2], the metric's single-GPU config): full DDM
-v=0.5 a=2 z=0.5 t=0.3 sv=sz=st=0.1 (reference test_models.py:18,71), HDDM's
-knobs err=1e-4 n_st=n_sz=2 adaptive simps_err=1e-3 w_outlier=0.1, p_outlier=0.05
-(base.py:688,713-716); 1M synthetic RTs per GPU sampled from the model with
-this package's gen_rts_from_cdf (density grid on the GPU, dt=1e-3).
+Workloads (BASELINE.json configs):
+  N = 1  C3: full DDM v=0.5 a=2 z=0.5 t=0.3 sv=sz=st=0.1 (reference
+         test_models.py:18,71), 1M trials resident on the GPU.
+  N > 1  C5: the same model, 100M trials in total sharded contiguously over the
+         N ranks (100M/N per GPU: 12.5M at N = 8), one RCCL all-reduce of
+         {sum log p, #zero trials, status} per call (scaling "strong").
+Knobs are HDDM's: err=1e-4, n_st=n_sz=2, adaptive, simps_err=1e-3,
+w_outlier=0.1, p_outlier=0.05 (base.py:688,713-716). RTs are sampled from the
+model by this package's gen_rts_from_cdf (density grid on the GPU, dt=1e-3).
 
 One step = one wiener_like call (wfpt.pyx:54-76 semantics) over the resident
-dataset: trial kernel + finalize + 16-byte result to the host; with N>1 ranks
-each rank owns 1M trials and the per-call exchange is one RCCL all-reduce
-(weak scaling). value = trials processed by all ranks / max-over-ranks time.
+shard. value = trials processed by all ranks / max-over-ranks time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
+
+With --gpus N > 1 and no WORLD_SIZE in the environment this process launches
+`torch.distributed.run` with N ranks itself (it never touches the GPU) and
+exits with the launcher's code.
 """
 import argparse
+import hashlib
 import json
-import math
 import os
+import subprocess
 import sys
 import time
 
@@ -30,9 +37,11 @@ METRIC = "trial-likelihood evals/sec (full DDM, sv/sz/st) at 1/2/4/8 GPUs"
 PARAMS = dict(v=0.5, sv=0.1, a=2.0, z=0.5, sz=0.1, t=0.3, st=0.1)
 KNOBS = dict(err=1e-4, n_st=2, n_sz=2, use_adaptive=1, simps_err=1e-3, w_outlier=0.1)
 P_OUTLIER = 0.05
-W_EVAL = 970.0   # FP64 VALU lane-ops per pdf_sv evaluation
-W_EPI = 99.0     # per-trial mixture + log + sum
-PEAK_LANE_OPS = 39.3e12  # 256 CU x 4 SIMD x 16 fp64 lanes/clk x 2.4 GHz (= 78.6 TFLOP/s FMA)
+C3_TRIALS = 1_000_000
+C5_TRIALS = 100_000_000
+# fp64 VALU peak: 256 CU x 4 SIMD x 16 fp64 lanes/clk x 2.4 GHz = 39.3e12 lane-ops/s
+# (the 78.6 TFLOP/s FMA-counted vector peak, MI355X_MICROARCH.md)
+PEAK_LANE_OPS = 39.3e12
 
 
 def args_tuple():
@@ -54,41 +63,84 @@ def make_rts(n, seed):
                                  samples=n, dt=1e-3)
 
 
+def host_threads():
+    """Host cores this process may use (the GPU box exports OMP_NUM_THREADS=16,
+    its CPU share per GPU; the machine has many more)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(x, budget_s):
-    """Reference CPU path on the host: oracle/_ref (the reference's own kernels
-    in its serial wiener_like loop) if present, else the C restatement."""
+    """The reference CPU path restated in C (oracle/wfpt_oracle.c, kind "port";
+    calibrated against the reference's own kernels in the build container:
+    profiles/r02/cpu_calibration.json), timed on this host's cores:
+    1 thread = the reference's serial wiener_like loop (wfpt.pyx:66-76);
+    all cores = the same per-trial full_pdf under OpenMP (the reference's
+    prange in pdf_array, wfpt.pyx:40, built with -fopenmp)."""
     import oracle
-    ref = oracle.load_ref()
-    kind = "reference" if ref is not None else "port"
-    fn = ref.wiener_like if ref is not None else oracle.wiener_like
-    sample = x[:50_000].copy()
+    kn = knobs_tuple()
+    one = x[:50_000].copy()
     done, t0 = 0, time.perf_counter()
     while True:
-        fn(sample, *args_tuple(), *knobs_tuple())
-        done += sample.size
-        el = time.perf_counter() - t0
-        if el >= budget_s:
+        oracle.wiener_like(one, *args_tuple(), *kn)
+        done += one.size
+        el1 = time.perf_counter() - t0
+        if el1 >= budget_s / 2:
             break
-    return {"value": done / el, "unit": "trials/s", "cores": 1, "kind": kind,
-            "sample": f"wiener_like over the first {sample.size} trials of the benchmark "
-                      f"dataset, repeated {done // sample.size}x ({el:.1f} s, 1 thread)"}
+    v1 = done / el1
+    nt = host_threads()
+    allc = x.copy()
+    done, t0 = 0, time.perf_counter()
+    while True:
+        lp = oracle.pdf_array(allc, *args_tuple(), kn[0], 1, kn[1], kn[2], kn[3], kn[4], kn[5],
+                              kn[6], n_threads=nt)
+        float(np.sum(lp))
+        done += allc.size
+        eln = time.perf_counter() - t0
+        if eln >= budget_s / 2:
+            break
+    vn = done / eln
+    return {"value": vn, "unit": "trials/s", "cores": nt, "kind": "port",
+            "value_1_thread": v1,
+            "sample": f"C restatement of wfpt.wiener_like (oracle/wfpt_oracle.c; port/reference "
+                      f"speed 1.01 measured in the build container): all {nt} host threads over "
+                      f"the {allc.size} benchmark trials x{done // allc.size} ({eln:.1f} s); "
+                      f"1 thread over the first {one.size} trials ({el1:.1f} s, "
+                      f"{v1:.3e} trials/s)"}
 
 
-def load_traffic(n_trials):
-    """HBM bytes per launch and VALU issue utilisation of the main kernel from
-    the committed rocprofv3 PMC summary (profiles/traffic.json), if present."""
+def pmc_summary(lib_path, n_trials):
+    """Executed-work figures of the dominant kernel from the committed rocprofv3
+    PMC summary (profiles/traffic.json, written by tools/summarize_profile.py),
+    used only if it was measured on this very library build and size."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
-        return None, None, None
+        return None
     try:
         with open(path) as fh:
             t = json.load(fh)
-        if int(t.get("n_trials", -1)) == int(n_trials):
-            return (float(t["hbm_bytes_per_launch"]), t.get("valu_issue_utilisation"),
-                    t.get("fp64_lane_ops_per_trial"))
     except Exception:
-        return None, None, None
-    return None, None, None
+        return None
+    with open(lib_path, "rb") as fh:
+        digest = hashlib.sha1(fh.read()).hexdigest()
+    t["matches_build"] = (t.get("lib_sha1") == digest and int(t.get("n_trials", -1)) == n_trials)
+    return t
+
+
+def launch_ranks(a):
+    """--gpus N > 1 without a torch.distributed environment: run this script
+    under torch.distributed.run with N ranks (one process per GPU)."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={a.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd)
 
 
 def main():
@@ -96,15 +148,18 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--trials", type=int, default=1_000_000, help="trials per GPU")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--trials", type=int, default=None,
+                    help="trials per GPU (default: C3 1M at N=1, C5 100M/N at N>1)")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
 
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world > 1:
+    if world != a.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={a.gpus}", file=sys.stderr)
     os.environ.setdefault("WFPT_DEVICE", str(local))
     from hddm_amd import _lib, wfpt
@@ -116,7 +171,13 @@ def main():
         pg = dist.group.WORLD
     ctx = _lib.context(local)
 
-    n = a.trials
+    c5 = world > 1
+    total = C5_TRIALS if c5 else C3_TRIALS
+    if a.trials is not None:
+        n = a.trials
+    else:
+        lo, hi = _lib.shard_range(total, world, rank)
+        n = hi - lo
     x = make_rts(n, 20261015 + rank)
     ds = wfpt.Dataset(x, device=local)
     if world > 1:
@@ -126,7 +187,7 @@ def main():
     else:
         step = lambda: ds.wiener_like(*args_tuple(), *knobs_tuple())
 
-    # untimed pass: count pdf_sv evaluations on this dataset (feeds W_trial)
+    # untimed pass: count pdf_sv evaluations on this dataset
     ctx.profile(ctx.PROF_EVALS)
     val = step()
     _, _, n_evals = ctx.profile_read(reset=True)
@@ -146,13 +207,10 @@ def main():
     for _ in range(a.steps):
         val = step()
     ctx.synchronize()
-    # each rank's clock stops when its own K calls are done (every call ends in
-    # the all-reduce, so ranks finish together); the closing barrier aligns the
-    # ranks for the next phase and the max over ranks below is the job time
     el = time.perf_counter() - t0
     barrier()
     # the same K calls again with HIP events recorded on the library's stream
-    # around the likelihood kernels of every call: per-launch kernel time
+    # around the dominant kernel (the level-0 pass): its per-launch duration
     ctx.profile(ctx.PROF_EVENTS)
     ctx.profile_read(reset=True)
     for _ in range(a.steps):
@@ -167,16 +225,27 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
 
-    total_trials = n * world * a.steps
-    value = total_trials / el
-    evals_per_trial = n_evals / n
-    w_trial = evals_per_trial * W_EVAL + W_EPI
+    glob = n * world
+    value = glob * a.steps / el
     k_avg_s = (k_ms / 1e3) / max(launches, 1)
-    achieved = n * w_trial / k_avg_s / 1e12
-    traffic, valu_util, f64_per_trial = load_traffic(n)
-    # hardware view: fp64 VALU lane-ops the kernel actually executes per trial
-    # (rocprofv3 SQ_INSTS_VALU_*_F64 x 64, profiles/traffic.json) over its time
-    exec_tops = n * f64_per_trial / k_avg_s / 1e12 if f64_per_trial else None
+    pmc = pmc_summary(_lib.LIB_PATH, n)
+    roof = {"bound": "valu-fp64", "peak": PEAK_LANE_OPS / 1e12, "unit": "T fp64-lane-ops/s",
+            "achieved": None, "frac": None, "traffic": None,
+            "kernel": "wfpt::fast_kernel<3, false, 0> (level-0 pass)",
+            "kernel_ms_avg": k_avg_s * 1e3, "kernel_launches": launches}
+    if pmc and pmc.get("matches_build"):
+        # executed fp64 VALU lane-ops per trial of this kernel (rocprofv3
+        # SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes, same build and dataset)
+        # over its live per-launch time
+        w = float(pmc["fp64_lane_ops_per_trial"])
+        achieved = n * w / k_avg_s / 1e12
+        roof.update(achieved=achieved, frac=achieved / (PEAK_LANE_OPS / 1e12),
+                    traffic=pmc.get("hbm_bytes_per_launch"), fp64_lane_ops_per_trial=w,
+                    valu_issue_utilisation=pmc.get("valu_issue_utilisation"),
+                    algorithmic_bytes=8.0 * n, pmc_source=pmc.get("source"))
+    else:
+        roof["note"] = ("profiles/traffic.json was not measured on this library build / size; "
+                        "run tools/gpu_profile.sh + tools/summarize_profile.py")
     out = {
         "metric": METRIC,
         "value": value,
@@ -186,31 +255,23 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": el / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if c5 else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (RTs sampled from the DDM by hddm_amd.wfpt.gen_rts_from_cdf, "
                 "seed 20261015+rank)",
-        "config": {"workload": "full DDM sv=sz=st=0.1 v=.5 a=2 z=.5 t=.3, HDDM knobs "
-                               "(err 1e-4, n_st=n_sz=2, adaptive, simps_err 1e-3), "
-                               "p_outlier .05; one wiener_like call per step",
-                   "trials_per_gpu": n, "global_trials": n * world,
+        "config": {"workload": ("C5: full DDM 100M trials sharded over %d GPUs + RCCL "
+                                "all-reduce" % world) if c5 else
+                               "C3: full DDM 1M trials on 1 GPU",
+                   "params": "sv=sz=st=0.1 v=.5 a=2 z=.5 t=.3, HDDM knobs (err 1e-4, "
+                             "n_st=n_sz=2, adaptive, simps_err 1e-3), p_outlier .05; one "
+                             "wiener_like call per step",
+                   "trials_per_gpu": n, "global_trials": glob,
                    "parallelism": f"trial-shard x{world}" + (" + RCCL all-reduce"
                                                               if world > 1 else ""),
-                   "pdf_sv_evals_per_trial": evals_per_trial,
+                   "pdf_sv_evals_per_trial": n_evals / n,
                    "logp": val},
-        "roofline": {"bound": "valu-fp64", "achieved": achieved, "peak": PEAK_LANE_OPS / 1e12,
-                     "unit": "T fp64-lane-ops/s", "frac": achieved / (PEAK_LANE_OPS / 1e12),
-                     "traffic": traffic,
-                     "kernel_ms_avg": k_avg_s * 1e3, "kernel_launches": launches,
-                     "w_trial_lane_ops": w_trial,
-                     # hardware view (rocprofv3 PMC, profiles/traffic.json): share of SIMD
-                     # cycles issuing VALU (4 cycles per wave64 fp64 op, 2 otherwise)
-                     "valu_issue_utilisation": valu_util,
-                     # frac above is algorithmic (the reference's op count, SURVEY.md
-                     # 8d); this is executed fp64 work over the same peak
-                     "executed_fp64": exec_tops,
-                     "executed_frac": exec_tops / (PEAK_LANE_OPS / 1e12) if exec_tops else None},
+        "roofline": roof,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(x, a.cpu_seconds)

@@ -4,9 +4,7 @@
 // pinned result slot, optional RCCL communicator), resident datasets, and the
 // call sequences  fast pass -> slow pass -> finalize  per likelihood. The last
 // kernel writes {sum, #zeros, status} straight into mapped pinned host memory
-// (no copy, no memset, no stream sync). Opt-in (WFPT_TAIL=1): a resident-data
-// wiener_like whose trials all finish in the fast pass is ONE kernel that
-// reduces and publishes itself (run_sum_tail); measured no faster, see DESIGN.
+// (no copy, no memset, no stream sync).
 // Calls into one context are serialised by its mutex; the ctypes binding
 // releases the GIL around every call.
 #include <hip/hip_runtime.h>
@@ -107,9 +105,6 @@ struct wfpt_ctx {
   DevBuf<double> mscal;
   DevBuf<unsigned char> wl;  // fast-pass worklists (lane ids per block)
   DevBuf<int> wl_n;          // deferred trials per block
-  DevBuf<unsigned> tk;       // fused-tail tickets: [0, g) per group, [g, g+2) top (0 at rest)
-  DevBuf<double> tpart;      // fused-tail per-block then per-group partial sums
-  DevBuf<int> tzero;         // fused-tail per-block then per-group zero counts
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
@@ -124,7 +119,6 @@ struct wfpt_ctx {
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
-  bool tail = false;           // WFPT_TAIL=1: one-kernel resident wiener_like (run_sum_tail)
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
@@ -143,11 +137,6 @@ struct wfpt_ds {
   int32_t* node = nullptr;
   int64_t* off = nullptr;
   int32_t n_nodes = 0;
-  // > 0: a recent fused-tail call on this dataset deferred trials, so the next
-  // `defers` calls enqueue the full fast -> slow -> finalize sequence up front
-  // (MCMC proposals move the parameters little: deferral persists), then the
-  // one-kernel path is tried again
-  mutable int defers = 0;
   // the last call on this dataset deferred no trial: the next one runs the
   // level-0 pass + finalize only (run_sum_fast), no slow pass
   mutable bool no_defer = false;
@@ -328,62 +317,6 @@ int read_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr
   return decode_sum(c, r, out, deferred);
 }
 
-// Resident-data sum as ONE kernel (fast_kernel<..., TAIL>; WFPT_TAIL=1): the
-// fast pass
-// reduces its own wave partials and publishes {sum, zeros, status} + the
-// completion word into mres. If it deferred trials it publishes only
-// seq | kDeferWord; the slow pass and finalize are then enqueued here (one
-// extra host round trip), and the dataset is marked so that its next call
-// enqueues all three kernels up front. Returns -1 when the tail path does not
-// apply (nothing launched), else a WFPT status with *out set on success.
-constexpr int kTailRetry = 32;
-
-int run_sum_tail(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
-                 double* out) {
-  const int64_t n = d->n;
-  if (!c->tail || c->count || n <= 0) return -1;
-  if (d->defers > 0) {
-    --d->defers;
-    return -1;
-  }
-  const int64_t ng = wfpt::tail_groups(n);
-  const int64_t nbk = wfpt::tail_blocks(n);
-  const int64_t nb = wfpt::partials_for(n, P, K);
-  HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
-  HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
-  if (int rc = reserve_worklist(c, n)) return rc;
-  if ((size_t)(ng + 2) > c->tk.cap) {
-    HIP_TRY(c->tk.reserve(ng + 2));
-    HIP_TRY(hipMemsetAsync(c->tk.p, 0, c->tk.cap * sizeof(unsigned), c->stream));
-  }
-  HIP_TRY(c->tpart.reserve(nbk + ng));
-  HIP_TRY(c->tzero.reserve(nbk + ng));
-  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  const unsigned long long seq = ++c->seq;
-  if (!wfpt::launch_sum_tail(d->x, n, P, K, c->part.p, c->zero.p, c->status, c->wl.p, c->wl_n.p,
-                             c->tk.p, c->tk.p + ng, c->tpart.p, c->tzero.p, c->tpart.p + nbk,
-                             c->tzero.p + nbk, c->mres_dev, seq, c->stream)) {
-    --c->seq;
-    return -1;
-  }
-  HIP_TRY(hipGetLastError());
-  if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  if (int rc = wait_word(c, c->mres + 3, ~wfpt::kDeferWord)) return rc;
-  const unsigned long long w = reinterpret_cast<const volatile unsigned long long*>(c->mres)[3];
-  if (w & wfpt::kDeferWord) {
-    d->defers = kTailRetry;
-    wfpt::launch_slow_pass(d->x, n, P, K, c->part.p, c->zero.p, c->status, c->wl.p, c->wl_n.p,
-                           c->stream);
-    HIP_TRY(hipGetLastError());
-    int64_t off = 0, cnt = 0;
-    wfpt::final_partials(n, P, K, &off, &cnt);
-    wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, c->mres_dev, ++c->seq,
-                          c->stream);
-    HIP_TRY(hipGetLastError());
-  }
-  return read_sum(c, c->mres, out);
-}
-
 // Resident-data sum predicted to defer nothing (the dataset's last call did
 // not): level-0 pass + finalize over its per-64-trial partials, no slow pass
 // (-4.6 us of empty slow kernel per call). If the level-0 pass did defer
@@ -453,7 +386,6 @@ int wfpt_open(int device, wfpt_ctx** out) {
   c->device = device;
   if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
-  if (const char* tm = std::getenv("WFPT_TAIL")) c->tail = std::strcmp(tm, "1") == 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -491,9 +423,6 @@ void wfpt_close(wfpt_ctx* c) {
   c->mscal.release();
   c->wl.release();
   c->wl_n.release();
-  c->tk.release();
-  c->tpart.release();
-  c->tzero.release();
   c->defer.release();
   c->nd_idx.release();
   c->nd_par.release();
@@ -602,9 +531,7 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  int rc = run_sum_tail(c, d, P, K, out);
-  if (rc >= 0) return rc;
-  rc = run_sum_fast(c, d, P, K, out);
+  int rc = run_sum_fast(c, d, P, K, out);
   if (rc >= 0) return rc;
   if (int rc2 = run_sum(c, d->x, d->n, P, K, c->mres_dev)) return rc2;
   bool deferred = true;

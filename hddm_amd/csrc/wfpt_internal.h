@@ -23,20 +23,6 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
                    hipEvent_t fast_done = nullptr);
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt);
-// Resident-data wiener_like as one fast kernel that also reduces and publishes
-// (fast_tail in wfpt_kernels.hip): out (mapped host) receives {sum, zeros,
-// status} and word seq, or only the word seq | kDeferWord when trials were
-// deferred — then launch_slow_pass + launch_finalize over final_partials finish
-// the call. grp: tail_groups(n) zeroed tickets; top: 2 zeroed words;
-// bpart/bzero: tail_blocks(n), gpart/gzero: tail_groups(n) entries. Returns
-// false (nothing launched) for n == 0 or fixed Simpson.
-constexpr unsigned long long kDeferWord = 1ull << 63;
-int64_t tail_blocks(int64_t n);
-int64_t tail_groups(int64_t n);
-bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                     int* zeros, int* status, unsigned char* wl, int* wl_n, unsigned* grp,
-                     unsigned* top, double* bpart, int* bzero, double* gpart, int* gzero,
-                     double* out, unsigned long long seq, hipStream_t s);
 void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                       int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s);
 // Status bit the level-0 pass of a sum sets when it deferred trials (besides

@@ -148,166 +148,17 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
   }
 }
 
-// Tail of the resident-data wiener_like (TAIL fast kernels): the call's
-// reduction and publication done by the fast kernel itself, so a call whose
-// trials all finish at level 0 is ONE kernel. Three levels, each "last to
-// arrive sums, in a fixed order":
-//   block: each wave leaves its partial in LDS and takes an LDS ticket; the
-//          last wave of the block sums the block's waves -> bpart[block];
-//   group: that wave takes the ticket of its group of 64 blocks; the last
-//          block of a group sums the group's 64 block partials -> gpart[g];
-//   top:   the last group sums the group partials (lane-strided) and, if no
-//          trial was deferred, writes {sum, #zeros, status} and then the
-//          completion word `seq` into the mapped result slot. Otherwise it
-//          writes seq | kDeferWord and the host runs slow_kernel +
-//          finalize_kernel (which fold the per-wave partials A.out[wave]).
-// Tickets and the deferred counter are reset by their last reader, so they are
-// zero at rest.
-//
-// Cross-XCD visibility without L2 write-backs: an agent-scope release fence
-// (__threadfence) flushes the XCD's whole L2 (buffer_wbl2); one per wave
-// measured +0.21 ms per 1M trials. Here the data handed between blocks is
-// stored and loaded with agent-scope relaxed atomics, which are coherent
-// across XCDs by themselves; the arriving wave waits for its stores to
-// complete (s_waitcnt 0) before it takes its ticket, and a reader issues its
-// loads only after its ticket said it was last. Only one wave per block pays
-// that round trip (one per wave measured +23 us per 1M trials).
-struct Tail {
-  unsigned* grp;       // per-group arrival tickets (ceil(nblocks / 64))
-  unsigned* top;       // [0] group ticket, [1] deferred-trial count
-  double* bpart;       // per-block partial sums
-  int* bzero;          // per-block zero counts
-  double* gpart;       // per-group partial sums
-  int* gzero;          // per-group zero counts
-  double* out;         // mapped result slot {sum, zeros, status, word}
-  int* status;
-  unsigned long long seq;
-};
-
-template <class T>
-__device__ inline void st_agent(T* p, T v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-template <class T>
-__device__ inline T ld_agent(const T* p) {
-  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// this wave's earlier stores have completed (vmcnt = expcnt = lgkmcnt = 0);
-// the signal fences keep the compiler from moving memory operations across it
-__device__ inline void stores_done() {
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_s_waitcnt(0);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-__device__ inline unsigned ticket(unsigned* p, unsigned v) {
-  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-struct TailLds {
-  double part[kFastBlock / 64];
-  int zero[kFastBlock / 64];
-  unsigned nslow;
-  unsigned cnt;
-};
-
-template <bool TAIL>
-__device__ inline void fast_tail(const TrialArgs& A, const Tail& T, TailLds& L, double lp, int zs,
-                                 int lane, int nslow) {
-  if (!TAIL) return;
-  constexpr int WPB = kFastBlock / 64;
-  const int w = threadIdx.x >> 6;
-  unsigned t = 0;
-  if (lane == 0) {
-    L.part[w] = lp;
-    L.zero[w] = zs;
-    if (nslow) atomicAdd(&L.nslow, (unsigned)nslow);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    t = atomicAdd(&L.cnt, 1u);
-  }
-  t = __shfl(t, 0, 64);
-  if (t != (unsigned)(WPB - 1)) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  const int64_t blk = blockIdx.x;
-  const int64_t nblk = gridDim.x;
-  const int64_t g = blk >> 6;
-  const int64_t ng = (nblk + 63) >> 6;
-  const int gsz = (int)((nblk - (g << 6)) < 64 ? (nblk - (g << 6)) : 64);
-  if (lane == 0) {
-    double s = 0.0;
-    int z = 0;
-    for (int k = 0; k < WPB; ++k) {
-      s += L.part[k];
-      z += L.zero[k];
-    }
-    st_agent(&T.bpart[blk], s);
-    st_agent(&T.bzero[blk], z);
-    if (L.nslow) ticket(&T.top[1], L.nslow);
-    stores_done();
-    t = ticket(&T.grp[g], 1u);
-  }
-  t = __shfl(t, 0, 64);
-  if (t != (unsigned)(gsz - 1)) return;
-  double s = 0.0;
-  int z = 0;
-  if (lane < gsz) {
-    s = ld_agent(&T.bpart[(g << 6) + lane]);
-    z = ld_agent(&T.bzero[(g << 6) + lane]);
-  }
-  s = wave_sum(s);
-  for (int o = 32; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
-  unsigned t2 = 0;
-  if (lane == 0) {
-    st_agent(&T.gpart[g], s);
-    st_agent(&T.gzero[g], z);
-    st_agent(&T.grp[g], 0u);
-    stores_done();
-    t2 = ticket(&T.top[0], 1u);
-  }
-  t2 = __shfl(t2, 0, 64);
-  if (t2 != (unsigned)(ng - 1)) return;
-  double s0 = 0.0, s1 = 0.0;
-  long long zz = 0;
-  int64_t j = lane;
-  for (; j + 64 < ng; j += 128) {
-    s0 += ld_agent(&T.gpart[j]);
-    s1 += ld_agent(&T.gpart[j + 64]);
-    zz += (long long)ld_agent(&T.gzero[j]) + ld_agent(&T.gzero[j + 64]);
-  }
-  if (j < ng) {
-    s0 += ld_agent(&T.gpart[j]);
-    zz += ld_agent(&T.gzero[j]);
-  }
-  s = wave_sum(s0 + s1);
-  zz = wave_sum_ll(zz);
-  if (lane == 0) {
-    const unsigned deferred = __hip_atomic_exchange(&T.top[1], 0u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-    st_agent(&T.top[0], 0u);
-    unsigned long long word = T.seq;
-    if (deferred == 0) {
-      T.out[0] = s;
-      T.out[1] = (double)zz;
-      T.out[2] = (double)atomicExch(T.status, 0);
-    } else {
-      word |= kDeferWord;
-    }
-    __threadfence_system();
-    reinterpret_cast<volatile unsigned long long*>(T.out)[3] = word;
-    __threadfence_system();
-  }
-}
-
 // Level-0 fast pass (MODE in kDirect..kAdaptTZ). Trials whose root Simpson
 // tests all pass are finished here; the others are compacted per WAVE into
 // `wl` (lane ids, one byte each, 64 slots per wave) and counted in
 // `wl_n[wave]` for slow_kernel. Barrier-free: every wave writes its own
 // partial sum / zero count (A.out[wave], A.zeros[wave]) and worklist, so a
-// wave that finishes early never waits for its block (TAIL: see fast_tail).
+// wave that finishes early never waits for its block.
 //
 // fast_chunk: one 64-trial chunk of the level-0 pass for the calling wave: trial
 // i = c*64 + lane with RT xi (ignored when i >= n). Writes the chunk's
 // worklist, partial sum and zero count; returns the wave-reduced partial (lp,
-// zs) and the deferred count for the fused tail.
+// zs) and the deferred count.
 template <int MODE, bool COUNT, int OUT>
 __device__ __forceinline__ void fast_chunk(const TrialArgs& A, unsigned char* wl, int* wl_n,
                                            int64_t c, int lane, double xi, double& lp_out,
@@ -362,17 +213,9 @@ __device__ __forceinline__ void fast_chunk(const TrialArgs& A, unsigned char* wl
   nslow_out = nslow;
 }
 
-template <int MODE, bool COUNT, int OUT, bool TAIL>
+template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
-  __shared__ TailLds L;
-  if (TAIL) {
-    if (threadIdx.x == 0) {
-      L.nslow = 0u;
-      L.cnt = 0u;
-    }
-    __syncthreads();
-  }
+void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
   // ascending |rt| in dispatch order: the costlier short-RT chunks start first
   // (dispatching largest |rt| first measured 3% slower)
   const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
@@ -380,7 +223,6 @@ void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n, Tail T) {
   double lp;
   int zs, nslow;
   fast_chunk<MODE, COUNT, OUT>(A, wl, wl_n, i >> 6, lane, i < A.n ? A.x[i] : 0.0, lp, zs, nslow);
-  if (OUT == OUT_SUM && !COUNT) fast_tail<TAIL>(A, T, L, lp, zs, lane, nslow);
 }
 
 // General pass over the trials the fast pass deferred. The fast pass leaves
@@ -773,8 +615,8 @@ static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned cha
   // both fast kernels leave one partial / worklist per 64 trials
   constexpr int TPB = 64;
   const int64_t nb = (n + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT, false>), dim3(fast_blocks(n)), dim3(kFastBlock), 0,
-                     s, A, wl, wl_n, Tail{});
+  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(n)), dim3(kFastBlock), 0,
+                     s, A, wl, wl_n);
   if (fast_done) (void)hipEventRecord(fast_done, s);
   if (MODE == kDirect) return;
   const int64_t g = slow_grid(nb);
@@ -880,27 +722,6 @@ static TrialArgs sum_args(const double* x, int64_t n, const Params& P, const Kno
   return A;
 }
 
-int64_t tail_blocks(int64_t n) { return fast_blocks(n); }
-int64_t tail_groups(int64_t n) { return (fast_blocks(n) + 63) / 64; }
-
-bool launch_sum_tail(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                     int* zeros, int* status, unsigned char* wl, int* wl_n, unsigned* grp,
-                     unsigned* top, double* bpart, int* bzero, double* gpart, int* gzero,
-                     double* out, unsigned long long seq, hipStream_t s) {
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  if (n <= 0 || mode > kAdaptTZ) return false;
-  const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
-  const Tail T{grp, top, bpart, bzero, gpart, gzero, out, status, seq};
-  const dim3 g(fast_blocks(n)), b(kFastBlock);
-  switch (mode) {
-    case kDirect: hipLaunchKernelGGL((fast_kernel<kDirect, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
-    case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
-    case kAdaptZ: hipLaunchKernelGGL((fast_kernel<kAdaptZ, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
-    default: hipLaunchKernelGGL((fast_kernel<kAdaptTZ, false, OUT_SUM, true>), g, b, 0, s, A, wl, wl_n, T); break;
-  }
-  return true;
-}
-
 bool launch_fast_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                       int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s,
                       hipEvent_t fast_done) {
@@ -909,9 +730,9 @@ bool launch_fast_pass(const double* x, int64_t n, const Params& P, const Knobs& 
   const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
   const dim3 g(fast_blocks(n)), b(kFastBlock);
   switch (mode) {
-    case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM, false>), g, b, 0, s, A, wl, wl_n, Tail{}); break;
-    case kAdaptZ: hipLaunchKernelGGL((fast_kernel<kAdaptZ, false, OUT_SUM, false>), g, b, 0, s, A, wl, wl_n, Tail{}); break;
-    default: hipLaunchKernelGGL((fast_kernel<kAdaptTZ, false, OUT_SUM, false>), g, b, 0, s, A, wl, wl_n, Tail{}); break;
+    case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM>), g, b, 0, s, A, wl, wl_n); break;
+    case kAdaptZ: hipLaunchKernelGGL((fast_kernel<kAdaptZ, false, OUT_SUM>), g, b, 0, s, A, wl, wl_n); break;
+    default: hipLaunchKernelGGL((fast_kernel<kAdaptTZ, false, OUT_SUM>), g, b, 0, s, A, wl, wl_n); break;
   }
   if (fast_done) (void)hipEventRecord(fast_done, s);
   return true;

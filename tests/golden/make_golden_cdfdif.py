@@ -76,6 +76,26 @@ def main(reference):
                         keys=np.array(["v", "sv", "a", "z", "sz", "t", "st", "p_outlier",
                                        "w_outlier"]))
     print("wrote", os.path.join(HERE, "cdfdif.npz"), P.shape, X.shape)
+    # random rows for the GPU tests (the reference never travels to the GPU box):
+    # tests/test_cdfdif.py::test_random_cdfdif_vs_reference and the stochastic hook
+    rng = np.random.default_rng(77)
+    RP, RX, RY = [], [], []
+    for _ in range(10):
+        p = [rng.uniform(-3, 3), rng.choice([0.0, rng.uniform(0, 2)]), rng.uniform(0.6, 2.0),
+             rng.uniform(0.4, 0.6), rng.choice([0.0, rng.uniform(0.05, 0.3)]),
+             rng.uniform(0.2, 0.45), rng.choice([0.0, rng.uniform(0.05, 0.3)]),
+             rng.choice([0.0, 0.05]), 0.1]
+        x = rng.choice([-1.0, 1.0], 2000) * (p[5] - p[6] / 2 + rng.gamma(1.5, 0.5, 2000))
+        x = np.clip(x, -4.9, 4.9)
+        RP.append(p)
+        RX.append(x)
+        RY.append(C.dmat_cdf_array(x, *p))
+    hook_p = np.array([0.7, 0.2, 1.8, 0.5, 0.1, 0.3, 0.1, 0.05, 0.1])
+    hook_x = np.linspace(-3, 3, 101)
+    np.savez_compressed(os.path.join(HERE, "cdfdif_random.npz"), params=np.array(RP),
+                        x=np.array(RX), y=np.array(RY), hook_params=hook_p, hook_x=hook_x,
+                        hook_y=C.dmat_cdf_array(hook_x, *hook_p))
+    print("wrote", os.path.join(HERE, "cdfdif_random.npz"))
 
 
 if __name__ == "__main__":

@@ -1,9 +1,10 @@
 """DMAT / Tuerlinckx CDF (§8(f) row 4): hddm_amd.cdfdif_wrapper.dmat_cdf_array vs
 the reference's own `cdfdif_wrapper` (src/cdfdif_wrapper.pyx:16-53, src/cdfdif.c).
 
-Fixtures: tests/golden/cdfdif.npz, generated from the reference extension by
-tests/golden/make_golden_cdfdif.py. On the GPU box oracle/_ref (built here)
-also provides the reference for random inputs.
+Fixtures: tests/golden/cdfdif.npz (branch-covering rows) and cdfdif_random.npz
+(random rows), both generated from the reference extension in the build
+container by tests/golden/make_golden_cdfdif.py; the reference itself never
+runs on the GPU box.
 
 Tolerance. The kernel keeps the reference's expression order; only libm vs
 OCML transcendental ulps differ. The reference evaluates F as a difference of
@@ -76,22 +77,31 @@ def test_golden_cdfdif_parity():
     print(f"cdfdif golden: max |dF| = {worst:.3e}")
 
 
-@pytest.mark.gpu
-def test_random_cdfdif_vs_reference():
+def _golden_random():
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cdfdif_random.npz")
+    return dict(np.load(d, allow_pickle=False))
+
+
+def test_random_fixture_pinned_to_reference():
+    """cdfdif_random.npz (the GPU tests' random cases) equals the reference extension."""
     import oracle
-    from hddm_amd import cdfdif_wrapper as cw
     C = oracle.load_ref_cdfdif()
     if C is None:
         pytest.skip("oracle/_ref/cdfdif_wrapper not built")
-    rng = np.random.default_rng(77)
-    for rep in range(10):
-        p = [rng.uniform(-3, 3), rng.choice([0.0, rng.uniform(0, 2)]), rng.uniform(0.6, 2.0),
-             rng.uniform(0.4, 0.6), rng.choice([0.0, rng.uniform(0.05, 0.3)]),
-             rng.uniform(0.2, 0.45), rng.choice([0.0, rng.uniform(0.05, 0.3)]),
-             rng.choice([0.0, 0.05]), 0.1]
-        x = rng.choice([-1.0, 1.0], 2000) * (p[5] - p[6] / 2 + rng.gamma(1.5, 0.5, 2000))
-        x = np.clip(x, -4.9, 4.9)
-        ref = C.dmat_cdf_array(x, *p)
+    g = _golden_random()
+    for p, x, y in zip(g["params"], g["x"], g["y"]):
+        np.testing.assert_array_equal(C.dmat_cdf_array(x, *p), y)
+    np.testing.assert_array_equal(C.dmat_cdf_array(g["hook_x"], *g["hook_params"]), g["hook_y"])
+
+
+@pytest.mark.gpu
+def test_random_cdfdif_vs_reference():
+    """Random parameter rows; expected values generated from the reference's own
+    extension in the build container (tests/golden/make_golden_cdfdif.py)."""
+    from hddm_amd import cdfdif_wrapper as cw
+    g = _golden_random()
+    for p, x, ref in zip(g["params"], g["x"], g["y"]):
         got = cw.dmat_cdf_array(x, *p)
         d = np.abs(got - ref)
         assert d.max() <= _tol(p), f"params {p}: max |dF| {d.max():.3e}"
@@ -115,14 +125,11 @@ def test_cdfdif_properties():
 @pytest.mark.gpu
 def test_stochastic_cdf_hook():
     """The node's `cdf` (likelihoods.py:90-91) is dmat_cdf_array with the class's w_outlier."""
-    import oracle
     from hddm_amd.likelihoods import generate_wfpt_stochastic_class
-    C = oracle.load_ref_cdfdif()
-    if C is None:
-        pytest.skip("oracle/_ref/cdfdif_wrapper not built")
+    g = _golden_random()
+    v, sv, a, z, sz, t, st, po, wo = g["hook_params"]
+    assert wo == 0.1  # the class's default w_outlier (base.py:716)
     cls = generate_wfpt_stochastic_class()
-    node = cls("wfpt", np.array([0.5, -0.8]), v=0.7, sv=0.2, a=1.8, z=0.5, sz=0.1, t=0.3,
-               st=0.1, p_outlier=0.05)
-    x = np.linspace(-3, 3, 101)
-    np.testing.assert_allclose(node.cdf(x), C.dmat_cdf_array(x, 0.7, 0.2, 1.8, 0.5, 0.1, 0.3,
-                                                             0.1, 0.05, 0.1), atol=CDF_ATOL)
+    node = cls("wfpt", np.array([0.5, -0.8]), v=v, sv=sv, a=a, z=z, sz=sz, t=t, st=st,
+               p_outlier=po)
+    np.testing.assert_allclose(node.cdf(g["hook_x"]), g["hook_y"], atol=CDF_ATOL)

@@ -334,69 +334,41 @@ def test_nodes_uniform_family_fast_path(gpu, oracle_lib, family):
             assert_total(got[j], terms, f"{family} node {j}")
 
 
-# --------------------------------------------------------------------------- fused tail
+# --------------------------------------------------------------------------- resident sizes
 
-@pytest.fixture(scope="module")
-def tail_ctx(gpu):
-    """A context opened with WFPT_TAIL=1 (the opt-in one-kernel resident path)."""
-    import os
-    from hddm_amd import _lib
-    old = os.environ.get("WFPT_TAIL")
-    os.environ["WFPT_TAIL"] = "1"
-    try:
-        c = _lib.Context(_lib.default_device())
-    finally:
-        if old is None:
-            del os.environ["WFPT_TAIL"]
-        else:
-            os.environ["WFPT_TAIL"] = old
-    yield c
-    c.close()
-
-
-def test_resident_one_kernel_tail(gpu, oracle_lib, tail_ctx):
-    """WFPT_TAIL=1: resident wiener_like runs as ONE kernel that reduces and
-    publishes its own result when no trial is deferred (run_sum_tail in
-    wfpt_capi.cpp); a deferring dataset falls back to fast -> slow -> finalize
-    for 32 calls, then retries. Sizes straddle the 256-trial block, the
-    64-block group and the 64-group final pass; repeated and interleaved calls
-    check that tickets are zero at rest."""
+def test_resident_sizes_and_repeats(gpu, oracle_lib):
+    """Resident wiener_like across sizes that straddle the 64-trial chunk, the
+    256-trial block and the finalize stride; repeated and interleaved calls
+    must return bit-identical totals (workspace words are zero at rest)."""
     rng = np.random.default_rng(20261016)
-    Dataset = lambda x: gpu.Dataset(x, ctx=tail_ctx)  # noqa: E731
     kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
     pinned = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
     stress = (-2.5, 2.2, 0.6, 0.45, 0.35, 0.25, 0.3)  # deep adaptive refinement
     sets = []
     for n in (1, 63, 64, 65, 255, 257, 16_383, 16_384, 16_385, 1_048_577, 1_100_001):
         x = rng.choice([-1.0, 1.0], n) * (0.3 + rng.gamma(2.0, 0.45, n))
-        sets.append((Dataset(x), x))
-    for args in (pinned, stress, (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0), (0.7, 0.4, 1.5, 0.5, 0.0, 0.3, 0.0)):
+        sets.append((gpu.Dataset(x), x))
+    for args in (pinned, stress, (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0),
+                 (0.7, 0.4, 1.5, 0.5, 0.0, 0.3, 0.0)):
         want = {}
         for ds, x in sets:
-            host = gpu.wiener_like(x, *args, *kn)  # host-array path: no tail
+            host = gpu.wiener_like(x, *args, *kn)
             got = ds.wiener_like(*args, *kn)
             if ds.n < 100_000:  # the big sizes: vs the (parity-tested) host path
                 ref = oracle_lib.pdf_array(x, *args, kn[0], 1, *kn[1:5], kn[5], kn[6])
-                assert_total(got, ref, f"tail n={ds.n} {args}")
+                assert_total(got, ref, f"resident n={ds.n} {args}")
             assert abs(got - host) <= 1e-11 * max(abs(host), 1.0), (ds.n, got, host)
             want[ds.n] = got
-        # interleaved repeats across datasets (40 > the 32-call fallback window)
         for rep in range(40):
             ds, _ = sets[rep % len(sets)]
-            got = ds.wiener_like(*args, *kn)
-            assert abs(got - want[ds.n]) <= 1e-13 * max(abs(want[ds.n]), 1.0), (rep, ds.n)
-    # semantics through the tail: a zero-density trial, NaN parameters
-    ds = Dataset(np.array([0.8, 0.1, -0.9] * 5000))
+            assert ds.wiener_like(*args, *kn) == want[ds.n], (rep, ds.n)
+    # semantics: a zero-density trial, NaN parameters (a == 0)
+    ds = gpu.Dataset(np.array([0.8, 0.1, -0.9] * 5000))
     assert ds.wiener_like(0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 1e-4) == -np.inf
     assert np.isfinite(ds.wiener_like(0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0, 1e-4, p_outlier=0.05))
     assert ds.wiener_like(0.5, 0.0, 0.0, 0.5, 0.0, 0.3, 0.0, 1e-4) == -np.inf  # zero beats NaN
-    assert np.isnan(Dataset(np.array([0.8, -0.9] * 5000)).wiener_like(
+    assert np.isnan(gpu.Dataset(np.array([0.8, -0.9] * 5000)).wiener_like(
         0.5, 0.0, 0.0, 0.5, 0.0, 0.3, 0.0, 1e-4))
-    # a deferred trial that overflows the Simpson stack still fails loudly
-    dso = Dataset(np.array([0.35, 0.9, -1.3]))
-    with pytest.raises(NotImplementedError):
-        dso.wiener_like(0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-10, n_st=40, n_sz=40, simps_err=0.0)
-    assert np.isfinite(dso.wiener_like(0.5, 0.3, 2.0, 0.5, 0.3, 0.3, 0.3, 1e-8))
 
 
 def test_resident_fast_only_prediction(gpu, oracle_lib):

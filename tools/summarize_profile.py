@@ -6,9 +6,14 @@ corrected as MI355X_MICROARCH.md §HBM prescribes: FETCH_SIZE (KiB) reads half
 the bytes of a wide coalesced stream on gfx950, so it is doubled; WRITE_SIZE
 (KiB) is taken as is.
 
-    python tools/summarize_profile.py r01 [--kernel 'void wfpt::trial_kernel<3, 0, false, 0>']
+    python tools/summarize_profile.py r02 [--kernel 'void wfpt::fast_kernel<3, false, 0>']
+
+traffic.json carries the sha1 of hddm_amd/lib/libwfpt_amd.so (the build that
+was shipped to the GPU box and profiled): bench.py uses the executed-work
+figures only while that build is the one it loads.
 """
 import argparse
+import hashlib
 import collections
 import csv
 import json
@@ -34,7 +39,7 @@ def per_launch(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="void wfpt::trial_kernel<3, 0, false, 0>")
+    ap.add_argument("--kernel", default="void wfpt::fast_kernel<3, false, 0>")
     ap.add_argument("--trials", type=int, default=1_000_000)
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "profiles", a.tag)
@@ -74,8 +79,14 @@ def main():
         json.dump(summary, fh, indent=1)
     shutil.copy(os.path.join(PROF, "trace", "trace_kernel_stats.csv"),
                 os.path.join(out_dir, "kernel_stats.csv"))
+    lib = os.path.join(ROOT, "hddm_amd", "lib", "libwfpt_amd.so")
+    with open(lib, "rb") as fh:
+        sha = hashlib.sha1(fh.read()).hexdigest()
+    summary["lib_sha1"] = sha
+    with open(os.path.join(out_dir, "pmc_summary.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
     with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as fh:
-        json.dump({"source": f"profiles/{a.tag}/pmc_summary.json", "kernel": a.kernel,
+        json.dump({"lib_sha1": sha, "source": f"profiles/{a.tag}/pmc_summary.json", "kernel": a.kernel,
                    "n_trials": a.trials, "hbm_bytes_per_launch": fetch_b + write_b,
                    "valu_issue_utilisation": summary["valu_issue_utilisation"],
                    "fp64_lane_ops_per_trial": summary["fp64_lane_ops_per_trial"],
