@@ -84,6 +84,7 @@ wfpt_profile_enable = _sig("wfpt_profile_enable", _I, [_VP, _I])
 wfpt_profile_read = _sig("wfpt_profile_read", _I,
                          [_VP, _PD, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I])
 wfpt_synchronize = _sig("wfpt_synchronize", _I, [_VP])
+wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
 EXPORTED = [
     "wfpt_device_count", "wfpt_open", "wfpt_close", "wfpt_last_error", "wfpt_dataset_create",
@@ -91,7 +92,20 @@ EXPORTED = [
     "wfpt_wiener_like_host", "wfpt_wiener_like_nodes", "wfpt_pdf_array", "wfpt_full_pdf",
     "wfpt_wiener_like_multi", "wfpt_dmat_cdf_array", "wfpt_comm_unique_id", "wfpt_comm_init",
     "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
+    "wfpt_decode_result",
 ]
+
+# error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)
+DEPTH_ERROR = 1.0
+BUDGET_ERROR = 1048576.0
+
+
+def decode_result(triple):
+    """The library's decode of a (rank-summed) {sum, zeros, errors} triple."""
+    r = (ctypes.c_double * 3)(*[float(v) for v in triple])
+    out = _D()
+    check(wfpt_decode_result(r, ctypes.byref(out)))
+    return out.value
 
 
 def check(rc):

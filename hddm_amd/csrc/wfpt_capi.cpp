@@ -25,6 +25,7 @@
 #include "wfpt_internal.h"
 
 static thread_local std::string g_last_error;
+extern "C" int wfpt_decode_result(const double r[3], double* out);
 
 static int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -103,8 +104,15 @@ struct wfpt_ctx {
   DevBuf<double> marr;    // wiener_like_multi parameter arrays
   DevBuf<double*> mptr;
   DevBuf<double> mscal;
-  DevBuf<unsigned char> wl;  // fast-pass worklists (lane ids per block)
-  DevBuf<int> wl_n;          // deferred trials per block
+  // deferred-trial state of adaptive calls (wfpt_internal.h: Work), sized for
+  // the largest call so far: slot-indexed, nslots = 64 * chunks
+  DevBuf<unsigned char> wl;  // lane of the deferred trial in each slot
+  DevBuf<int> wl_n;          // per chunk: #tree | #exact << 8
+  DevBuf<int> rflag;         // per slot: kFlag*
+  DevBuf<double> tf;         // per slot: tree sample values (SoA)
+  DevBuf<int> rcnt;          // per slot: evaluation counts (PROF_EVALS only)
+  DevBuf<uint32_t> tasks;    // tree-level task lists
+  int* ntask = nullptr;      // device: 8 task counters (0 at rest)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
@@ -112,9 +120,9 @@ struct wfpt_ctx {
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
-  double* mres = nullptr;      // mapped pinned {sum, zeros, status}: finalize writes it
+  double* mres = nullptr;      // mapped pinned {sum, zeros, errors, deferred, word}
   double* mres_dev = nullptr;  // its device alias
-  unsigned long long seq = 0;  // completion word finalize writes to mres[3]
+  unsigned long long seq = 0;  // completion word finalize writes to mres[4]
   MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
@@ -196,54 +204,77 @@ int fetch_status(wfpt_ctx* c) {
   HIP_TRY(hipMemsetAsync(c->status, 0, sizeof(int), c->stream));  // 0 at rest
   return WFPT_OK;
 }
-int check_status_value(double st);
-int check_status(wfpt_ctx* c) { return check_status_value((double)(*c->host_status & 3)); }
+int check_status_value(double enc);
+// the raw device flag word (kFlagDepth | kFlagBudget) in the encoded form
+double encode_status(int st) {
+  return (double)(st & wfpt::kFlagDepth) + ((st & wfpt::kFlagBudget) ? wfpt::kBudgetUnit : 0.0);
+}
+int check_status(wfpt_ctx* c) { return check_status_value(encode_status(*c->host_status)); }
 
-// Worklists: one byte per trial slot and one count per fast block; blocks own
-// 256 trials (1-D kernels) or 64 (outer-t split), so size for the finer one.
-int reserve_worklist(wfpt_ctx* c, int64_t n) {
-  const int64_t nb64 = (n + 63) / 64;
-  HIP_TRY(c->wl.reserve(std::max<int64_t>(nb64 * 64 + 256, 1)));
-  HIP_TRY(c->wl_n.reserve(std::max<int64_t>(nb64, 1)));
+// Deferred-trial state for adaptive calls over up to n trials (grow-only).
+int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
+  const int64_t nw = std::max<int64_t>((n + 63) / 64, 1);
+  const int64_t ns = nw * 64;
+  HIP_TRY(c->wl.reserve(ns));
+  HIP_TRY(c->wl_n.reserve(nw));
+  HIP_TRY(c->rflag.reserve(ns));
+  HIP_TRY(c->tf.reserve(ns * wfpt::kTreePoints));
+  HIP_TRY(c->tasks.reserve(wfpt::task_capacity(ns)));
+  if (c->count) HIP_TRY(c->rcnt.reserve(ns));
+  W->wl = c->wl.p;
+  W->wl_n = c->wl_n.p;
+  W->rflag = c->rflag.p;
+  W->F = c->tf.p;
+  W->rcnt = c->count ? c->rcnt.p : nullptr;
+  W->tasks = c->tasks.p;
+  W->ntask = c->ntask;
+  W->nslots = ns;
   return WFPT_OK;
 }
 
 // Status words are 0 at rest: finalize_kernel resets the device flag after
-// reporting it, and the other paths clear it before their launch.
-int check_status_value(double st) {
-  const int s = (int)st;
-  if (s == 0) return WFPT_OK;
-  if (s == 1)
-    return fail(WFPT_ERR_UNSUPPORTED,
-                "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
-                    std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)");
-  if (s == 2)
-    return fail(WFPT_ERR_UNSUPPORTED,
-                "a trial exceeded WFPT_EVAL_BUDGET pdf_sv evaluations (raise simps_err)");
-  return fail(WFPT_ERR_UNSUPPORTED, "Simpson depth / evaluation budget exceeded (status " +
-                                        std::to_string(s) + ", summed over ranks)");
+// reporting it, and the other paths clear it before their launch. enc:
+// #depth errors + kBudgetUnit * #budget errors (summed over ranks).
+int check_status_value(double enc) {
+  if (enc == 0) return WFPT_OK;
+  const double budget = std::floor(enc / wfpt::kBudgetUnit);
+  const double depth = enc - budget * wfpt::kBudgetUnit;
+  std::string msg;
+  if (depth > 0)
+    msg = "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
+          std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)";
+  if (budget > 0) {
+    if (!msg.empty()) msg += "; ";
+    msg += "a trial exceeded WFPT_EVAL_BUDGET pdf_sv evaluations (raise simps_err)";
+  }
+  return fail(WFPT_ERR_UNSUPPORTED, msg);
 }
 
-// Fast pass (+ slow pass) + finalize over device x[n]; the 3-double result
-// {sum, zeros, status} lands in `out` (mapped host memory or device).
+// Likelihood sum over device x[n]: adaptive / direct families run the level-0
+// pass and (part & kPassDeferred) the deferred-trial pass, fixed Simpson one
+// trial kernel; then finalize writes {sum, zeros, errors, deferred} + the
+// completion word to `out` (mapped host memory or device).
 int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
-            const wfpt::Knobs& K, double* out, int keep = -1) {
+            const wfpt::Knobs& K, double* out, int part = wfpt::kPassAll) {
   const int64_t nb = wfpt::partials_for(n, P, K);
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
-  if (int rc = reserve_worklist(c, n)) return rc;
-  if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
-  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  wfpt::Work W;
+  if (int rc = reserve_work(c, n, &W)) return rc;
+  const bool adaptive = wfpt::has_deferred_pass(P, K);
+  if (c->count && (part & wfpt::kPassFast))
+    HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   // profiling: ev0..ev1 bracket the level-0 fast kernel (the dominant kernel,
   // the one rocprofv3 reports as fast_kernel<...>)
-  wfpt::launch_trials(0, dx, n, P, K, c->part.p, c->zero.p, c->count ? c->evals : nullptr,
-                      c->status, 0, c->wl.p, c->wl_n.p, c->stream,
-                      c->profile ? c->ev1 : nullptr);
+  const bool prof = c->profile && (part & wfpt::kPassFast);
+  if (prof) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  wfpt::launch_trials(0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p, c->zero.p,
+                      c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
+                      prof ? c->ev1 : nullptr);
   HIP_TRY(hipGetLastError());
-  int64_t off = 0, cnt = 0;
-  wfpt::final_partials(n, P, K, &off, &cnt);
-  wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, out, ++c->seq,
-                        c->stream, keep);
+  const int64_t nw = (n + 63) / 64;
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? W.wl_n : nullptr, adaptive ? nw : 0,
+                        c->status, out, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -269,12 +300,12 @@ int finish_profile(wfpt_ctx* c) {
 // asked whether it failed; after 5 s, or if the stream is idle without the
 // word, it falls back to a stream sync so a device error is reported, never a
 // stale number.
-int wait_word(wfpt_ctx* c, const void* word, unsigned long long mask = ~0ull) {
+int wait_word(wfpt_ctx* c, const void* word) {
   if (c->spin) {
     const volatile unsigned long long* w = reinterpret_cast<const volatile unsigned long long*>(word);
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
-      if ((w[0] & mask) == c->seq) {
+      if (w[0] == c->seq) {
         std::atomic_thread_fence(std::memory_order_acquire);
         if (c->profile) HIP_TRY(hipEventSynchronize(c->ev1));
         return WFPT_OK;
@@ -283,32 +314,29 @@ int wait_word(wfpt_ctx* c, const void* word, unsigned long long mask = ~0ull) {
         const hipError_t q = hipStreamQuery(c->stream);
         if (q != hipSuccess && q != hipErrorNotReady)
           return fail(WFPT_ERR_HIP, std::string("likelihood kernels: ") + hipGetErrorString(q));
-        if (q == hipSuccess && (w[0] & mask) != c->seq) break;  // idle: let the stream sync decide
+        if (q == hipSuccess && w[0] != c->seq) break;  // idle: let the stream sync decide
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
       }
     }
   }
   HIP_TRY(hipStreamSynchronize(c->stream));
-  if ((*reinterpret_cast<const volatile unsigned long long*>(word) & mask) != c->seq)
+  if (*reinterpret_cast<const volatile unsigned long long*>(word) != c->seq)
     return fail(WFPT_ERR_HIP, "the call's completion word was not written");
   return WFPT_OK;
 }
 
 int wait_result(wfpt_ctx* c, const double* r) {
-  if (r == c->mres) return wait_word(c, r + 3);
+  if (r == c->mres) return wait_word(c, r + 4);
   HIP_TRY(hipStreamSynchronize(c->stream));
   return WFPT_OK;
 }
 
-// Decodes {sum, zeros, status} from host memory `r` of a finished call;
-// *deferred (if given) = the level-0 pass deferred trials.
+// Decodes {sum, zeros, errors, deferred} from host memory `r` of a finished
+// call; *deferred (if given) = the level-0 pass deferred trials.
 int decode_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr) {
-  const int st = (int)r[2];
-  if (deferred) *deferred = (st & wfpt::kStatusDeferred) != 0;
-  if (int rc = check_status_value((double)(st & ~wfpt::kStatusDeferred))) return rc;
-  if (int rc = finish_profile(c)) return rc;
-  *out = (r[1] > 0) ? -INFINITY : r[0];
-  return WFPT_OK;
+  if (deferred) *deferred = r[3] != 0.0;
+  if (int rc = wfpt_decode_result(r, out)) return rc;
+  return finish_profile(c);
 }
 
 // Waits for the call and decodes its result.
@@ -318,39 +346,21 @@ int read_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr
 }
 
 // Resident-data sum predicted to defer nothing (the dataset's last call did
-// not): level-0 pass + finalize over its per-64-trial partials, no slow pass
-// (-4.6 us of empty slow kernel per call). If the level-0 pass did defer
-// trials this time (kStatusDeferred in the result), the slow pass and a second
-// finalize run over the intact partials and worklists, so the result is always
-// the full one; only that call pays a host round trip. Returns -1 when the
-// path does not apply (nothing launched).
+// not): level-0 pass + finalize only (no deferred-trial kernels). If the pass
+// did defer trials this time (finalize reports it), the deferred pass and a
+// second finalize run over the intact chunk partials, giving the same result
+// bit for bit as the full sequence; only that call pays a host round trip.
+// Returns -1 when the path does not apply (nothing launched).
 int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
                  double* out) {
   const int64_t n = d->n;
-  if (c->count || !d->no_defer || n <= 0) return -1;
-  const int64_t nb = wfpt::partials_for(n, P, K);
-  HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
-  HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
-  if (int rc = reserve_worklist(c, n)) return rc;
-  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  if (!wfpt::launch_fast_pass(d->x, n, P, K, c->part.p, c->zero.p, c->status, c->wl.p, c->wl_n.p,
-                              c->stream, c->profile ? c->ev1 : nullptr))
-    return -1;
-  HIP_TRY(hipGetLastError());
-  const int64_t nw = (n + 63) / 64;
-  wfpt::launch_finalize(c->part.p, c->zero.p, nw, c->status, c->mres_dev, ++c->seq, c->stream);
-  HIP_TRY(hipGetLastError());
+  if (c->count || !d->no_defer || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
+  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassFast)) return rc;
   if (int rc = wait_result(c, c->mres)) return rc;
-  if (((int)c->mres[2] & wfpt::kStatusDeferred) == 0) return decode_sum(c, c->mres, out);
+  if (c->mres[3] == 0.0) return decode_sum(c, c->mres, out);
   d->no_defer = false;
-  wfpt::launch_slow_pass(d->x, n, P, K, c->part.p, c->zero.p, c->status, c->wl.p, c->wl_n.p,
-                         c->stream);
-  HIP_TRY(hipGetLastError());
-  int64_t off = 0, cnt = 0;
-  wfpt::final_partials(n, P, K, &off, &cnt);
-  wfpt::launch_finalize(c->part.p + off, c->zero.p + off, cnt, c->status, c->mres_dev, ++c->seq,
-                        c->stream);
-  HIP_TRY(hipGetLastError());
+  if (int rc = check_status_value(c->mres[2])) return rc;
+  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassDeferred)) return rc;
   return read_sum(c, c->mres, out);
 }
 
@@ -366,6 +376,13 @@ int upload(wfpt_ctx* c, const double* x, int64_t n) {
 extern "C" {
 
 const char* wfpt_last_error(void) { return g_last_error.c_str(); }
+
+int wfpt_decode_result(const double r[3], double* out) {
+  if (!r || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (int rc = check_status_value(r[2])) return rc;
+  *out = (r[1] > 0) ? -INFINITY : r[0];  // any zero-density trial: -inf (wfpt.pyx:71-72)
+  return WFPT_OK;
+}
 
 int wfpt_device_count(int* n) {
   if (!n) return fail(WFPT_ERR_ARG, "null pointer");
@@ -395,11 +412,14 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->host_status, sizeof(int), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemset(c->status, 0, sizeof(int));
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&c->mres, 4 * sizeof(double),
+    e = hipHostMalloc((void**)&c->mres, 5 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->ntask, 8 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->ntask, 0, 8 * sizeof(int));
+  if (e == hipSuccess) std::memset(c->mres, 0, 5 * sizeof(double));
   if (e != hipSuccess) {
     wfpt_close(c);
     return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
@@ -423,6 +443,11 @@ void wfpt_close(wfpt_ctx* c) {
   c->mscal.release();
   c->wl.release();
   c->wl_n.release();
+  c->rflag.release();
+  c->tf.release();
+  c->rcnt.release();
+  c->tasks.release();
+  if (c->ntask) (void)hipFree(c->ntask);
   c->defer.release();
   c->nd_idx.release();
   c->nd_par.release();
@@ -568,9 +593,10 @@ int wfpt_pdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p
   if (int rc = upload(c, x, n)) return rc;
   HIP_TRY(c->lp.reserve(n));
   if (int rc = begin_status(c)) return rc;
-  if (int rc = reserve_worklist(c, n)) return rc;
-  wfpt::launch_trials(1, c->x.p, n, P, K, c->lp.p, nullptr, nullptr, c->status, logp == 1,
-                      c->wl.p, c->wl_n.p, c->stream);
+  wfpt::Work W;
+  if (int rc = reserve_work(c, n, &W)) return rc;
+  wfpt::launch_trials(1, wfpt::kPassAll, c->x.p, n, P, K, c->lp.p, nullptr, nullptr, c->status,
+                      logp == 1, W, c->stream);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   if (int rc = fetch_status(c)) return rc;
@@ -675,7 +701,8 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   wfpt::launch_multi(c->x.p, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
                      c->status, c->stream);
   HIP_TRY(hipGetLastError());
-  wfpt::launch_finalize(c->part.p, c->zero.p, nb, c->status, c->mres_dev, ++c->seq, c->stream);
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, nullptr, 0, c->status, c->mres_dev, ++c->seq,
+                        c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
   if (int rc = check_status_value(c->mres[2])) return rc;
@@ -760,11 +787,11 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  HIP_TRY(c->res.reserve(3));
-  // the deferred-trials bit is per rank: keep it out of the summed status
-  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p, ~wfpt::kStatusDeferred)) return rc;
-  // {sum, zeros, status} of every rank summed: any zero trial or failure anywhere
-  // reaches every rank
+  HIP_TRY(c->res.reserve(5));
+  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p)) return rc;
+  // {sum, zeros, encoded errors} of every rank summed: any zero trial or
+  // failure anywhere reaches every rank (the error encoding keeps depth and
+  // budget failures apart under the sum, wfpt_internal.h: kBudgetUnit)
   NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 3, ncclDouble, ncclSum, c->comm, c->stream));
   // the summed result goes to the mapped slot with a fresh completion word
   // (run_sum's finalize used the previous one for the device copy)

@@ -4,18 +4,25 @@
 // for one-trial-per-lane execution:
 //   * every *decision* (series branch, term count K, adaptive stop test, node
 //     coordinates) is computed with the same IEEE operations in the same order
-//     as the reference, so the quadrature tree is identical;
+//     as the reference, so the quadrature tree is identical; a stop test
+//     decided within kTieBand of its threshold, and a density that hinges on
+//     subnormal rounding, send the trial to the exact path (wfpt_exact.hpp);
 //   * work that depends only on the non-decision time node t (the series
 //     branch and K, sqrt/log terms, sv normalisers) is hoisted out of the z
 //     integral: one `TNode` per t node serves all z nodes;
-//   * the reference's recursion becomes an explicit per-lane stack (registers
-//     for depth <= 4, scratch beyond) driven by a loop with a single
-//     evaluation site, so divergent refinement does not duplicate code.
+//   * the root level of every adaptive Simpson runs in the level-0 pass
+//     (fast_level0); deeper tree levels run breadth-first over all deferred
+//     trials (TreeFn / tree_node / tree_value, wfpt_kernels.hip), beyond
+//     kBfDepth on a per-lane walk with an explicit stack (adaptive_walk).
 // Compiled with -ffp-contract=off: no FMA contraction, like the x86-64 build
 // of the reference.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include "../../include/wfpt_amd.h"
+#include "wfpt_crlibm.hpp"
+#include "wfpt_exact.hpp"
 
 #pragma clang fp contract(off)
 
@@ -56,28 +63,39 @@ __host__ __device__ inline int select_mode(double sz, double st, int use_adaptiv
 }
 
 // ---------------------------------------------------------------------------
+// Routing of trials whose value hinges on last-bit rounding (wfpt_exact.hpp).
+//
+// kExactBelow: a trial density below it (or zero, negative, NaN) is recomputed
+// on the exact path: there intermediate values can be subnormal, where one
+// rounding is up to 1e-5 relative, and a zero / negative / NaN outcome is a
+// decision, not a rounding.
+// kTieBand: an adaptive stop test |S2 - S| <= 15 err decided within this
+// relative band of its threshold sends the trial to the exact path (the fast
+// path's node values carry ~1e-14 relative error; the band is 1000x wider).
+constexpr double kExactBelow = 1e-290;
+constexpr double kTieBand = 1e-11;
+enum Flag : int {
+  kFlagDepth = 1,     // refinement deeper than the stack (WFPT_MAX_DEPTH)
+  kFlagBudget = 2,    // more than kEvalBudget pdf_sv evaluations in one trial
+  kFlagExact = 4,     // recompute on the exact path
+  kFlagFallback = 8,  // tree deeper than the breadth-first levels: per-lane walk
+};
+constexpr int kFlagErrors = kFlagDepth | kFlagBudget;
+
+
+// ---------------------------------------------------------------------------
 // Per-t-node quantities of ftt_01w / pdf_sv that do not depend on w (= z).
 //
 // Decisions (pos, small/large branch, K) are computed with the reference's
 // exact operations. Values use cheaper equivalent forms whose rounding differs
-// by a few ulp (WFPT_EXACT_MATH=1 restores the literal expression order):
+// by a few ulp (trials whose value hinges on last-bit rounding are sent to the
+// exact path, wfpt_exact.hpp):
 //   * exp(-k^2 pi^2 tt/2) = q^(k^2), q = exp(-pi^2 tt/2), by two products per k;
 //   * sin(k pi w) by the Chebyshev recurrence from one sincospi(w);
 //   * exp(log p + c) = p * exp(c)  (overflow of exp(c) falls back to the
 //     literal form; p < 0 keeps the reference's NaN from log);
 //   * divisions by per-node constants become multiplications by reciprocals.
-#ifndef WFPT_EXACT_MATH
-#define WFPT_EXACT_MATH 0
-#endif
-// WFPT_SUBNORMAL_GUARD=1: where a value enters the subnormal range, take the
-// literal reference expression (one subnormal ulp can be a 1e-5 relative
-// change of a density below DBL_MIN). Off by default: such densities are
-// compared on the subnormal grid (|dp| <= 8 ulps), see tests/test_gpu_parity.py.
-#ifndef WFPT_SUBNORMAL_GUARD
-#define WFPT_SUBNORMAL_GUARD 0
-#endif
 constexpr double kDblMin = 2.2250738585072014e-308;
-constexpr double kSubnormalLo = -745.2, kSubnormalHi = -708.3;  // exp() subnormal band
 
 // sin(pi w) and cos(pi w) for w in [0, 1] (the only range full_pdf produces:
 // validity + flip keep every z node in [0, 1]). Exact reduction t = 2w,
@@ -131,12 +149,13 @@ struct TNode {
   int K;        // number of series terms (pdf.pxi:52, 60)
   int small;    // 1 => small-time series
   int pos;      // xx > 0 (else density 0, pdf.pxi:92)
+  int amb;      // the decision sits within 1e-12 of a threshold: exact path
 };
 
 // Series branch and term count of one t node (pdf.pxi:36-60): small-time
 // series iff ks < kl, K = ceil(min). kl and ks feed ONLY these two decisions.
 struct Decision {
-  int small, K;
+  int small, K, amb;
 };
 
 // fp32 estimate of the decision (~1e-7 relative). Returns false — the caller
@@ -175,10 +194,14 @@ __device__ inline bool decide32(double tt, double err, Decision& D, float& args_
   if (rng || Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k) return false;
   D.small = ksf < klf;
   D.K = (int)ceilf(kk);
+  D.amb = 0;
   return true;
 }
 
-// The reference's fp64 operations (pdf.pxi:36-60).
+// The reference's fp64 operations (pdf.pxi:36-60), reached when the fp32
+// estimate is within 1e-5 of a threshold. OCML's log differs from glibc's by
+// <= 1 ulp, so a decision within 1e-12 (relative) of a threshold is marked
+// ambiguous and the trial goes to the exact path (glibc-equal log).
 __device__ inline Decision decide64(double tt, double err) {
   double kl, ks;
   const double sqt = sqrt(tt);
@@ -200,7 +223,11 @@ __device__ inline Decision decide64(double tt, double err) {
   }
   Decision D;
   D.small = ks < kl;
-  D.K = (int)ceil(D.small ? ks : kl);
+  const double kk = D.small ? ks : kl;
+  D.K = (int)ceil(kk);
+  constexpr double tol = 1e-12;
+  D.amb = fabs(arg_l - 1.0) <= tol || fabs(arg_s - 1.0) <= tol || fabs(ks - kl) <= tol * kl ||
+          fabs(kk - rint(kk)) <= tol * kk;
   return D;
 }
 
@@ -209,7 +236,7 @@ __device__ inline Decision decide64(double tt, double err) {
 // node's decision, established by the caller (shared over a trial's t grid).
 __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err,
                                     double qhint = -1.0, bool has_known = false,
-                                    Decision known = Decision{0, 0}) {
+                                    Decision known = Decision{0, 0, 0}) {
   TNode T;
   T.xx = xx;
   T.pos = xx > 0;
@@ -222,6 +249,7 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   T.vvx = 0.0;
   T.K = 0;
   T.small = 0;
+  T.amb = 0;
   if (!T.pos) return T;
   const double a2 = a * a;
   const double tt = xx / a2;
@@ -229,15 +257,12 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   Decision D;
   float args;
   if (has_known) D = known;
-  else if (WFPT_EXACT_MATH || !decide32(tt, err, D, args)) D = decide64(tt, err);
+  else if (!decide32(tt, err, D, args)) D = decide64(tt, err);
+  T.amb = D.amb;
   if (D.small) {
     T.small = 1;
     T.K = D.K;
-#if WFPT_EXACT_MATH
-    T.rn = 1.0 / sqrt((2.0 * kPi) * ((tt * tt) * tt));
-#else
     T.rn = rsqrt((2.0 * kPi) * ((tt * tt) * tt));  // value only: 1/sqrt(2 pi tt^3)
-#endif
     T.m = -0.5 / tt;
   } else {
     T.small = 0;
@@ -245,13 +270,6 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
     T.m = qhint >= 0.0 ? qhint : exp((-kPi2 * tt) / 2.0);
     T.q2 = T.m * T.m;
   }
-#if WFPT_EXACT_MATH
-  T.sc = 1.0 / a2;
-  if (sv != 0) {
-    T.cden = 1.0 / (((2.0 * (sv * sv)) * xx) + 2.0);
-    T.sc = T.sc / sqrt(((sv * sv) * xx) + 1.0);
-  }
-#else
   // values only: 1/(2u) and 1/(a^2 sqrt(u)), u = sv^2 xx + 1, from one rsqrt
   T.sc = 1.0 / a2;
   if (sv != 0) {
@@ -259,7 +277,6 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
     T.cden = (0.5 * r) * r;
     T.sc = T.sc * r;
   }
-#endif
   T.vvx = (v * v) * xx;
   return T;
 }
@@ -273,27 +290,10 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
     const int upper = (int)ceil((K - 1) / 2.);
     for (int k = lower; k <= upper; ++k) {
       const double wk = w + (double)(2 * k);
-#if WFPT_EXACT_MATH
-      p = p + wk * exp(((-(wk * wk)) / 2.0) / T.tt);
-#else
-      double arg = (wk * wk) * T.m;
-      if (WFPT_SUBNORMAL_GUARD && arg < kSubnormalHi && arg > kSubnormalLo)
-        arg = ((-(wk * wk)) / 2.0) / T.tt;  // subnormal term: the reference's rounding
-      p = p + wk * exp(arg);
-#endif
+      p = p + wk * exp((wk * wk) * T.m);
     }
-#if WFPT_EXACT_MATH
-    p = p / sqrt((2.0 * kPi) * pow(T.tt, 3.0));
-#else
     p = p * T.rn;
-#endif
   } else {
-#if WFPT_EXACT_MATH
-    for (int k = 1; k <= K; ++k) {
-      const double dk = (double)k;
-      p = p + (dk * exp((((-(dk * dk)) * kPi2) * T.tt) / 2.0)) * sin((dk * kPi) * w);
-    }
-#else
     double s1, c1;
     sincospi01(w, s1, c1);
     const double tc = c1 + c1;
@@ -308,7 +308,6 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
       r = r * T.q2;
       p = p + ((double)k * e) * sk;
     }
-#endif
     p = p * kPi;
   }
   return p;
@@ -318,115 +317,39 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
 __device__ inline double tnode_pdf_sv(const TNode& T, double w, double v, double sv, double a) {
   if (!T.pos) return 0.0;
   const double p = tnode_ftt(T, w);
-#if WFPT_EXACT_MATH
-  if (sv == 0) return (p * exp((((-v) * a) * w) - (T.vvx / 2.))) / (a * a);
-  const double azsv = (a * w) * sv;
-  return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) /
-                          (((2.0 * (sv * sv)) * T.xx) + 2.0)) /
-          sqrt(((sv * sv) * T.xx) + 1.0)) /
-         (a * a);
-#else
   if (sv == 0) {
     const double ex = exp((((-v) * a) * w) - (T.vvx * 0.5));
-    const double r = (p * ex) * T.sc;
-    if (WFPT_SUBNORMAL_GUARD && fabs(r) < kDblMin && r != 0) return (p * ex) / (a * a);
-    return r;
+    return (p * ex) * T.sc;
   }
   if (p < 0) return __builtin_nan("");  // log(p < 0) in the reference
   const double azsv = (a * w) * sv;
   const double c = (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) * T.cden;
   const double ec = exp(c);
   const double r = (p * ec) * T.sc;
-  if (__builtin_isinf(ec) || (WFPT_SUBNORMAL_GUARD && r < kDblMin && r != 0))  // literal form
+  if (__builtin_isinf(ec))  // exp(c) overflow: the literal form
     return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) /
                              (((2.0 * (sv * sv)) * T.xx) + 2.0)) /
             sqrt(((sv * sv) * T.xx) + 1.0)) /
            (a * a);
   return r;
-#endif
 }
 
-// pdf_sv at N z nodes of ONE t node. The nodes share the series branch and
-// K (they depend on tt only), so the N evaluations run as N independent,
-// interleavable instruction chains under one control flow, sharing the
-// q^(k^2) recurrence and every constant. Same arithmetic as tnode_pdf_sv.
-template <int N>
-__device__ inline void tnode_pdf_sv_n(const TNode& T, const double (&w)[N], double v, double sv,
-                                      double a, double (&out)[N]) {
-  double p[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) p[i] = 0.0;
-  if (!T.pos) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = 0.0;
-    return;
-  }
-  const int K = T.K;
-  if (T.small) {
-    const int lower = (int)(-floor((K - 1) / 2.));
-    const int upper = (int)ceil((K - 1) / 2.);
-    for (int k = lower; k <= upper; ++k) {
-      const double k2 = (double)(2 * k);
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const double wk = w[i] + k2;
-        p[i] = p[i] + wk * exp((wk * wk) * T.m);
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) p[i] = p[i] * T.rn;
-  } else {
-    double tc[N], sk[N], skm1[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      double s1, c1;
-      sincospi01(w[i], s1, c1);
-      tc[i] = c1 + c1;
-      sk[i] = s1;
-      skm1[i] = 0.0;
-      if (K >= 1) p[i] = T.m * s1;
-    }
-    double e = T.m, r = T.m * T.q2;
-    for (int k = 2; k <= K; ++k) {
-      e = e * r;
-      r = r * T.q2;
-      const double ke = (double)k * e;
-#pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const double sn = tc[i] * sk[i] - skm1[i];
-        skm1[i] = sk[i];
-        sk[i] = sn;
-        p[i] = p[i] + ke * sk[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) p[i] = p[i] * kPi;
-  }
-  if (sv == 0) {
-#pragma unroll
-    for (int i = 0; i < N; ++i)
-      out[i] = (p[i] * exp((((-v) * a) * w[i]) - (T.vvx * 0.5))) * T.sc;
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const double azsv = (a * w[i]) * sv;
-    const double c = (((azsv * azsv) - (((2.0 * a) * v) * w[i])) - T.vvx) * T.cden;
-    const double ec = exp(c);
-    double r2 = (p[i] * ec) * T.sc;
-    if (p[i] < 0) r2 = __builtin_nan("");  // log(p < 0) in the reference
-    out[i] = r2;
-  }
-  // exp(c) overflow: the reference's literal exp(log p + c) (rare, per lane)
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, w[i], v, sv, a);
-  }
-}
-
-__device__ inline double pdf_sv(double xx, double v, double sv, double a, double w, double err) {
+__device__ inline double pdf_sv(double xx, double v, double sv, double a, double w, double err,
+                                int& flags) {
   const TNode T = tnode_setup(xx, v, sv, a, err);
+  if (T.amb) flags |= kFlagExact;
   return tnode_pdf_sv(T, w, v, sv, a);
+}
+
+
+// ---------------------------------------------------------------------------
+// The reference's stop test of adaptiveSimpsonsAux (integrate.pxi:105 / 170):
+// true = refine. Marks kFlagExact when the test is decided inside kTieBand.
+__device__ inline bool simpson_refine(double S, double S2, double err, int bottom, int& flags) {
+  if (bottom <= 0) return false;
+  const double d = fabs(S2 - S), thr = 15 * err;
+  if (fabs(d - thr) <= kTieBand * ((fabs(S) + fabs(S2)) + thr)) flags |= kFlagExact;
+  return !(d <= thr);
 }
 
 // ---------------------------------------------------------------------------
@@ -478,25 +401,26 @@ struct MemStack {
   __device__ inline void set_left(int i, double v) { f[i].left = v; }
 };
 
-// Integrates g over [lb0, ub0] exactly like adaptiveSimpsons_1D/_2D followed by
-// adaptiveSimpsonsAux(_2D): g(c) must already include the division by ZT (or st).
-// Every lane walks its own quadrature tree; each loop trip evaluates g at the 3
-// initial nodes or at the 2 new nodes of one interval, from ONE call site.
-// A refinement deeper than the stack capacity (overflow |= 1) or a trial
-// exceeding kEvalBudget pdf_sv evaluations (overflow |= 2) abandons the trial
-// at once: the call then fails with WFPT_ERR_UNSUPPORTED instead of returning
-// a number, and no input can keep a wave busy without bound.
 constexpr long long kEvalBudget = 1ll << 24;
 
+// Integrates g over [lb0, ub0] exactly like adaptiveSimpsons_1D/_2D followed by
+// adaptiveSimpsonsAux(_2D): g(c) must already include the division by ZT (or
+// st). With init == false the walk starts at the aux node (lb0, ub0, S0, fb0,
+// fe0, fm0) instead (a refinement resumed from known values). Every lane walks
+// its own tree; each loop trip evaluates g at the 3 prologue nodes or the 2
+// new nodes of one interval from ONE call site. Depth past the stack, the
+// evaluation budget or a near-tie stop test abandon the trial (flags set,
+// NaN returned): no input keeps a wave busy without bound.
 template <class Stack, class G>
-__device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double err0,
-                                          int depth, int& overflow, const long long& ne) {
+__device__ inline double adaptive_walk(G&& g, double lb0, double ub0, double err0, int depth,
+                                       int& flags, const long long& ne, bool init = true,
+                                       double S0 = 0.0, double fb0 = 0.0, double fe0 = 0.0,
+                                       double fm0 = 0.0) {
   Stack stk;
   double lb = lb0, ub = ub0, err = err0;
-  double S = 0.0, fb = 0.0, fe = 0.0, fm = 0.0;
+  double S = S0, fb = fb0, fe = fe0, fm = fm0;
   int bottom = depth, sp = 0;
   unsigned right_mask = 0u;  // bit i: frame i has finished its left child
-  bool init = true;
   double result = 0.0;
   for (;;) {
     const double c = (ub + lb) / 2.;
@@ -512,8 +436,8 @@ __device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double 
       else if (i == 1) y1 = y;
       else y2 = y;
     }
-    if (ne > kEvalBudget) overflow |= 2;
-    if (overflow) {
+    if (ne > kEvalBudget) flags |= kFlagBudget;
+    if (flags & (kFlagErrors | kFlagExact)) {
       result = __builtin_nan("");
       break;
     }
@@ -531,9 +455,13 @@ __device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double 
     const double Sl = (h / 12) * ((fb + (4 * fd)) + fm);
     const double Sr = (h / 12) * ((fm + (4 * fee)) + fe);
     const double S2 = Sl + Sr;
-    const bool refine = !(bottom <= 0 || fabs(S2 - S) <= 15 * err);
+    const bool refine = simpson_refine(S, S2, err, bottom, flags);
+    if (flags & kFlagExact) {
+      result = __builtin_nan("");
+      break;
+    }
     if (refine && sp >= Stack::kCap) {
-      overflow |= 1;
+      flags |= kFlagDepth;
       result = __builtin_nan("");
       break;
     }
@@ -591,10 +519,9 @@ __device__ inline double adaptive_simpson(G&& g, double lb0, double ub0, double 
 
 // Fixed composite Simpson, integrate.pxi:12-45. Returns the integral; the
 // reference leaves `y` uninitialised when n == 0 (0 here).
-template <bool COUNT>
 __device__ inline double simpson_1d(double x, double v, double sv, double a, double z, double t,
                                     double err, double lb_z, double ub_z, int n_sz, double lb_t,
-                                    double ub_t, int n_st, long long& ne) {
+                                    double ub_t, int n_st, long long& ne, int& flags) {
   double ht, hz;
   const int n = (n_st < n_sz) ? n_sz : n_st;
   if (n_st == 0) {
@@ -609,13 +536,13 @@ __device__ inline double simpson_1d(double x, double v, double sv, double a, dou
     ub_z = z;
   }
   ++ne;
-  double S = pdf_sv(x - lb_t, v, sv, a, lb_z, err);
+  double S = pdf_sv(x - lb_t, v, sv, a, lb_z, err, flags);
   double y = 0.0;
   for (int i = 1; i <= n; ++i) {
     const double z_tag = lb_z + hz * i;
     const double t_tag = lb_t + ht * i;
     ++ne;
-    y = pdf_sv(x - t_tag, v, sv, a, z_tag, err);
+    y = pdf_sv(x - t_tag, v, sv, a, z_tag, err, flags);
     if (i & 1) S += (4 * y);
     else S += (2 * y);
   }
@@ -624,16 +551,15 @@ __device__ inline double simpson_1d(double x, double v, double sv, double a, dou
   return ((ht + hz) * S) / 3;
 }
 
-template <bool COUNT>
 __device__ inline double simpson_2d(double x, double v, double sv, double a, double z, double t,
                                     double err, double lb_z, double ub_z, int n_sz, double lb_t,
-                                    double ub_t, int n_st, long long& ne) {
+                                    double ub_t, int n_st, long long& ne, int& flags) {
   const double ht = (ub_t - lb_t) / n_st;
-  double S = simpson_1d<COUNT>(x, v, sv, a, z, lb_t, err, lb_z, ub_z, n_sz, 0, 0, 0, ne);
+  double S = simpson_1d(x, v, sv, a, z, lb_t, err, lb_z, ub_z, n_sz, 0, 0, 0, ne, flags);
   double y = 0.0;
   for (int i_t = 1; i_t <= n_st; ++i_t) {
     const double t_tag = lb_t + ht * i_t;
-    y = simpson_1d<COUNT>(x, v, sv, a, z, t_tag, err, lb_z, ub_z, n_sz, 0, 0, 0, ne);
+    y = simpson_1d(x, v, sv, a, z, t_tag, err, lb_z, ub_z, n_sz, 0, 0, 0, ne, flags);
     if (i_t & 1) S += (4 * y);
     else S += (2 * y);
   }
@@ -642,94 +568,143 @@ __device__ inline double simpson_2d(double x, double v, double sv, double a, dou
   return (ht * S) / 3;
 }
 
-// full_pdf (pdf.pxi:104-146) for one trial. MODE is the launch-uniform
-// integration family (kRuntime: decided per lane).
-template <int MODE, class Stack, bool COUNT>
-__device__ inline double full_pdf(double x, const Params& P, const Knobs& K, long long& ne,
-                                  int& ovf) {
-  const double a = P.a, sv = P.sv, t = P.t;
+// full_pdf's prologue (pdf.pxi:111-125): validity, boundary flip, |x|, the
+// st / sz < 1e-3 zeroing. valid == 0: density 0 (pdf.pxi:111-113).
+struct Trial {
+  double x, v, z, sz, st;
+  int valid;
+};
+
+__device__ inline Trial trial_setup(double x, const Params& P) {
+  Trial T;
   double v = P.v, z = P.z, st = P.st, sz = P.sz;
-  if ((z < 0) || (z > 1) || (a < 0) || (t < 0) || (st < 0) || (sv < 0) || (sz < 0) ||
-      (sz > 1) || ((fabs(x) - (t - st / 2.)) < 0) || (z + sz / 2. > 1) || (z - sz / 2. < 0) ||
-      (t - st / 2. < 0))
-    return 0.0;
+  const double a = P.a, sv = P.sv, t = P.t;
+  T.valid = !((z < 0) || (z > 1) || (a < 0) || (t < 0) || (st < 0) || (sv < 0) || (sz < 0) ||
+              (sz > 1) || ((fabs(x) - (t - st / 2.)) < 0) || (z + sz / 2. > 1) ||
+              (z - sz / 2. < 0) || (t - st / 2. < 0));
   if (x > 0) {
     v = -v;
     z = 1. - z;
   }
-  x = fabs(x);
+  T.x = fabs(x);
   if (st < 1e-3) st = 0;
   if (sz < 1e-3) sz = 0;
+  T.v = v;
+  T.z = z;
+  T.st = st;
+  T.sz = sz;
+  return T;
+}
+
+// full_pdf (pdf.pxi:104-146) for one trial: the general per-lane walk (the
+// fallback for trees deeper than the breadth-first levels, fixed Simpson,
+// per-trial parameters). MODE is the integration family (kRuntime: per lane).
+template <int MODE, class Stack>
+__device__ inline double full_pdf(double x0, const Params& P, const Knobs& K, long long& ne,
+                                  int& flags) {
+  const Trial tr = trial_setup(x0, P);
+  if (!tr.valid) return 0.0;
+  const double a = P.a, sv = P.sv, t = P.t;
+  const double x = tr.x, v = tr.v, z = tr.z, st = tr.st, sz = tr.sz;
   const int mode = (MODE == kRuntime) ? select_mode(sz, st, K.use_adaptive) : MODE;
   const double err = K.err;
 
   if (mode == kDirect) {
     ++ne;
-    return pdf_sv(x - t, v, sv, a, z, err);
+    return pdf_sv(x - t, v, sv, a, z, err, flags);
   }
   if (mode == kAdaptZ) {
     // adaptiveSimpsons_1D over z at fixed t: one t node for every evaluation
     const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
-    const double ZT = ub_z - lb_z;
-    const double iZT = 1.0 / ZT;
+    const double iZT = 1.0 / (ub_z - lb_z);
     const TNode T = tnode_setup(x - t, v, sv, a, err);
+    if (T.amb) flags |= kFlagExact;
     auto g = [&](double zc) -> double {
       ++ne;
-      return WFPT_EXACT_MATH ? tnode_pdf_sv(T, zc, v, sv, a) / ZT
-                             : tnode_pdf_sv(T, zc, v, sv, a) * iZT;
+      return tnode_pdf_sv(T, zc, v, sv, a) * iZT;
     };
-    return adaptive_simpson<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, ovf, ne);
+    return adaptive_walk<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, flags, ne);
   }
   if (mode == kAdaptT) {
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
-    const double ZT = ub_t - lb_t;
-    const double iZT = 1.0 / ZT;
+    const double iZT = 1.0 / (ub_t - lb_t);
     auto g = [&](double tc) -> double {
       ++ne;
-      return WFPT_EXACT_MATH ? pdf_sv(x - tc, v, sv, a, z, err) / ZT
-                             : pdf_sv(x - tc, v, sv, a, z, err) * iZT;
+      return pdf_sv(x - tc, v, sv, a, z, err, flags) * iZT;
     };
-    return adaptive_simpson<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, ovf, ne);
+    return adaptive_walk<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, flags, ne);
   }
   if (mode == kAdaptTZ) {
     const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
-    const double ZT = ub_z - lb_z;
-    const double stw = ub_t - lb_t;  // `st` of adaptiveSimpsons_2D (integrate.pxi:187)
-    const double iZT = 1.0 / ZT, istw = 1.0 / stw;
-    const double e1 = K.simps_err;
-    const int nsz = K.n_sz;
+    const double iZT = 1.0 / (ub_z - lb_z), istw = 1.0 / (ub_t - lb_t);
     auto outer = [&](double tc) -> double {
       const TNode T = tnode_setup(x - tc, v, sv, a, err);
+      if (T.amb) flags |= kFlagExact;
       auto inner = [&](double zc) -> double {
         ++ne;
-        return WFPT_EXACT_MATH ? tnode_pdf_sv(T, zc, v, sv, a) / ZT
-                               : tnode_pdf_sv(T, zc, v, sv, a) * iZT;
+        return tnode_pdf_sv(T, zc, v, sv, a) * iZT;
       };
-      const double r = adaptive_simpson<Stack>(inner, lb_z, ub_z, e1, nsz, ovf, ne);
-      return WFPT_EXACT_MATH ? r / stw : r * istw;
+      return adaptive_walk<Stack>(inner, lb_z, ub_z, K.simps_err, K.n_sz, flags, ne) * istw;
     };
-    return adaptive_simpson<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, ovf, ne);
+    return adaptive_walk<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, flags, ne);
   }
   if (mode == kFixedT)
-    return simpson_1d<COUNT>(x, v, sv, a, z, t, err, z, z, 0, t - st / 2., t + st / 2., K.n_st,
-                             ne);
+    return simpson_1d(x, v, sv, a, z, t, err, z, z, 0, t - st / 2., t + st / 2., K.n_st, ne,
+                      flags);
   if (mode == kFixedZ)
-    return simpson_1d<COUNT>(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz, t, t, 0,
-                             ne);
-  return simpson_2d<COUNT>(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz,
-                           t - st / 2., t + st / 2., K.n_st, ne);
+    return simpson_1d(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz, t, t, 0, ne,
+                      flags);
+  return simpson_2d(x, v, sv, a, z, t, err, z - sz / 2., z + sz / 2., K.n_sz, t - st / 2.,
+                    t + st / 2., K.n_st, ne, flags);
+}
+
+// The exact path for one trial (wfpt_exact.hpp), out of line: the kernels call
+// it only for the rare trials routed there, and it must not add to their
+// register allocation. Returns the density; flags gets kFlagDepth/Budget.
+__device__ __noinline__ double exact_pdf(double x, Params P, Knobs K, long long* ne, int* flags) {
+  wfpt_x::Ctx C;
+  const double p = wfpt_x::full_pdf(x, P.v, P.sv, P.a, P.z, P.sz, P.t, P.st, K.err, K.n_st,
+                                    K.n_sz, K.use_adaptive, K.simps_err, C);
+  *ne += C.ne;
+  *flags |= C.ovf;
+  return p;
+}
+
+// The general per-lane walk, out of line (trees deeper than the breadth-first
+// levels); a near-tie on it goes to the exact path.
+template <int MODE>
+__device__ __noinline__ double fallback_pdf(double x, Params P, Knobs K, long long* ne,
+                                            int* flags) {
+  long long n = 0;
+  int f = 0;
+  double p = full_pdf<MODE, MemStack<WFPT_MAX_DEPTH>>(x, P, K, n, f);
+  if (f & kFlagExact) {
+    n = 0;
+    f = 0;
+    p = exact_pdf(x, P, K, &n, &f);
+  }
+  *ne += n;
+  *flags |= f;
+  return p;
+}
+
+// Settles a trial density: a value that hinges on last-bit rounding (zero,
+// negative, NaN, below kExactBelow, or kFlagExact raised on the way: a
+// near-tie or an ambiguous series decision) is recomputed on the exact path,
+// unless it is a structural zero (invalid parameters, or no evaluation point
+// with x - t_node > 0: no arithmetic produced it).
+__device__ inline double settle(double p, double x, const Params& P, const Knobs& K, bool structural,
+                                long long& ne, int& flags) {
+  if (!(flags & kFlagExact) && (p > kExactBelow || structural)) return p;
+  flags &= ~kFlagExact;
+  long long n = 0;
+  const double q = exact_pdf(x, P, K, &n, &flags);
+  ne = n;
+  return q;
 }
 
 // ---------------------------------------------------------------------------
-// Level-0 fast path. Most trials stop at the root interval of every adaptive
-// Simpson they run (the pinned HDDM workload: exactly 25 pdf_sv evaluations
-// per trial). fast_pdf computes exactly that part of the reference's
-// quadrature tree (prologue + root aux node, integrate.pxi:114-141 /
-// 181-206), with one evaluation site and no stacks, and reports `slow` when
-// any root test asks for refinement; such trials are recomputed by the
-// general kernel (full_pdf above). MODE: kDirect, kAdaptT, kAdaptZ, kAdaptTZ.
-
 // Per-trial part of the root-level z grid. The 5 z nodes (lb, d, c, e, ub of
 // integrate.pxi:114-141 / 143-178) are the same for every t node of a trial,
 // so everything that depends on z alone is computed once per trial:
@@ -769,8 +744,8 @@ __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, d
   return G;
 }
 
-// pdf_sv at the 5 root-level z nodes of one t node (same values as
-// tnode_pdf_sv_n<5> to a few ulp):
+// pdf_sv at the 5 root-level z nodes of one t node (the values of
+// tnode_pdf_sv at each node to a few ulp):
 //   * small-t series: the exponents (g_j + 2k)^2 m are quadratic in j on the
 //     equally spaced grid, so per term k two exponentials (j = 0 and the first
 //     ratio) and one shared second-difference factor replace five; exponents
@@ -778,12 +753,7 @@ __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, d
 //   * large-t series: the Chebyshev recurrence in k from the rotated sin/cos;
 //   * the drift factor exp(c_j): three exponentials and the second-difference
 //     recurrence (direct exps when |c| > 600).
-#ifdef WFPT_EXP_NOINLINE
-__device__ __attribute__((noinline))
-#else
-__device__ inline
-#endif
-void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
+__device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
                                           double a, double (&out)[5]) {
   double p[5];
 #pragma unroll
@@ -912,126 +882,378 @@ void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
     if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, G.g[i], v, sv, a);
 }
 
-// Root-level adaptive Simpson over z at a fixed t node: 5 evaluations, run
-// 5-wide on the equally spaced grid (they share the t node's branch and K).
-__device__ inline double level0_z(const TNode& T, const ZGrid& G, double iZT, double serr,
-                                  int depth, double v, double sv, double a, bool& slow) {
+// ---------------------------------------------------------------------------
+// Level-0 pass and breadth-first tree levels (adaptive modes).
+//
+// Node order used below: lb, d, c, e, ub of an interval (integrate.pxi:114-141
+// prologue nodes lb, c, ub + the root aux nodes d, e).
+
+// A deferred trial keeps its tree's sample values at the dyadic points of the
+// root interval, kTreeW + 1 of them, in a slot-indexed structure-of-arrays
+// F[point * nslots + slot]; levels 1..kBfDepth are evaluated breadth-first
+// over all deferred trials (wfpt_kernels.hip: level_kernel). Deeper trees
+// continue on the per-lane walk (kFlagFallback).
+#ifndef WFPT_BF_DEPTH
+#define WFPT_BF_DEPTH 2
+#endif
+constexpr int kBfDepth = WFPT_BF_DEPTH;
+constexpr int kTreeW = 4 << kBfDepth;
+constexpr int kTreePoints = kTreeW + 1;
+
+// Level-L task lists, levels 1..kBfDepth back to back: level l holds up to
+// 2^l tasks per slot.
+__host__ __device__ inline int64_t task_offset(int L, int64_t nslots) {
+  return ((int64_t(1) << L) - 2) * nslots;
+}
+__host__ __device__ inline int64_t task_capacity(int64_t nslots) {
+  return ((int64_t(1) << (kBfDepth + 1)) - 2) * nslots;
+}
+
+// kFall: continue the whole trial on the per-lane walk (a z tree deeper than
+// kInnerCap inside a t tree).
+enum Outcome : int { kFinal = 0, kTree = 1, kExact = 2, kFall = 3 };
+
+// The reference's Simpson estimates of one interval from its 5 values.
+struct Simp {
+  double S, Sl, Sr, S2;
+};
+__device__ inline Simp simp5(double h, double fb, double fd, double fm, double fe, double fu) {
+  Simp s;
+  s.S = (h / 6) * ((fb + (4 * fm)) + fu);
+  s.Sl = (h / 12) * ((fb + (4 * fd)) + fm);
+  s.Sr = (h / 12) * ((fm + (4 * fe)) + fu);
+  s.S2 = s.Sl + s.Sr;
+  return s;
+}
+
+// The z integral at one t node (adaptiveSimpsons_1D over z, integrate.pxi:
+// 114-141), root level only: the root's 5 evaluations 5-wide on the grid and
+// its stop test. repair = the test asks for refinement (the value is then the
+// root estimate; the caller recomputes the node with inner_full after its
+// main loop, where few registers are live).
+__device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, double v,
+                                    double sv, double a, const Knobs& K, int& flags,
+                                    long long& ne, bool& repair) {
   double f[5];
   tnode_pdf_sv_grid5(T, G, v, sv, a, f);
 #pragma unroll
-  for (int i = 0; i < 5; ++i) f[i] = f[i] * iZT;
-  // reference names: f_beg = f[0], f_end = f[4], f_mid = f[2], fd = f[1], fe = f[3]
-  const double h = G.g[4] - G.g[0];
-  const double S = (h / 6) * ((f[0] + (4 * f[2])) + f[4]);
-  const double Sl = (h / 12) * ((f[0] + (4 * f[1])) + f[2]);
-  const double Sr = (h / 12) * ((f[2] + (4 * f[3])) + f[4]);
-  const double S2 = Sl + Sr;
-  if (!(depth <= 0 || fabs(S2 - S) <= 15 * serr)) slow = true;
-  return S2 + (S2 - S) / 15;
+  for (int i = 0; i < 5; ++i) f[i] = f[i] * iZz;
+  ne += 5;
+  const Simp s = simp5(G.g[4] - G.g[0], f[0], f[1], f[2], f[3], f[4]);
+  repair = simpson_refine(s.S, s.S2, K.simps_err, K.n_sz, flags);
+  return s.S2 + (s.S2 - s.S) / 15;
 }
 
-template <int MODE>
-__device__ inline double fast_pdf(double x, const Params& P, const Knobs& K, bool& slow,
-                                  int& valid) {
-  const double a = P.a, sv = P.sv, t = P.t;
-  double v = P.v, z = P.z, st = P.st, sz = P.sz;
-  if ((z < 0) || (z > 1) || (a < 0) || (t < 0) || (st < 0) || (sv < 0) || (sz < 0) ||
-      (sz > 1) || ((fabs(x) - (t - st / 2.)) < 0) || (z + sz / 2. > 1) || (z - sz / 2. < 0) ||
-      (t - st / 2. < 0)) {
-    valid = 0;
+// The complete z integral at one t node (root + refinement), inline and
+// register-light: a per-lane walk with a kInnerCap-frame register stack
+// (n_sz <= kInnerCap; deeper z trees go to the per-lane fallback with the
+// whole trial, kFlagFallback). Counts its root evaluations again.
+constexpr int kInnerCap = 3;
+__device__ inline double inner_full(const TNode& T, double lbz, double ubz, double iZz, double v,
+                                    double sv, double a, const Knobs& K, int& flags,
+                                    long long& ne) {
+  if (K.n_sz > kInnerCap) {
+    flags |= kFlagFallback;
     return 0.0;
   }
-  valid = 1;
-  if (x > 0) {
-    v = -v;
-    z = 1. - z;
-  }
-  x = fabs(x);
-  if (st < 1e-3) st = 0;
-  if (sz < 1e-3) sz = 0;
-  const double err = K.err;
-  if (MODE == kDirect) return pdf_sv(x - t, v, sv, a, z, err);
-  if (MODE == kAdaptZ) {
-    const double lb = z - sz / 2., ub = z + sz / 2.;
-    const ZGrid G = zgrid_setup(lb, ub, v, sv, a);
-    const TNode T = tnode_setup(x - t, v, sv, a, err);
-    return level0_z(T, G, 1.0 / (ub - lb), K.simps_err, K.n_sz, v, sv, a, slow);
-  }
-  // t outer: kAdaptT (one evaluation per t node) or kAdaptTZ (a z integral per t node)
-  const double lb = t - st / 2., ub = t + st / 2.;
-  const double c = (ub + lb) / 2.;
-  const double d = (lb + c) / 2., e = (c + ub) / 2.;
-  const double lbz = z - sz / 2., ubz = z + sz / 2.;
-  const double iZz = (MODE == kAdaptTZ) ? 1.0 / (ubz - lbz) : 0.0;
-  const double iZt = 1.0 / (ub - lb);
-  ZGrid G;
-  if (MODE == kAdaptTZ) G = zgrid_setup(lbz, ubz, v, sv, a);
-  // large-time factor q = exp(-pi^2 (x - tc) / (2 a^2)) over the t grid:
-  // q(lb + k (ub - lb) / 4) = q(lb) R^k with R = exp(pi^2 (ub - lb) / (8 a^2))
-  // (values only; direct exps where the products leave the safe range)
-  double qn[5] = {-1.0, -1.0, -1.0, -1.0, -1.0};
-  {
-    const double a2 = a * a;
-    const double q0 = exp((-kPi2 * ((x - lb) / a2)) / 2.0);
-    const double R = exp((kPi2 * (ub - lb)) / (8.0 * a2));
-    if (!WFPT_EXACT_MATH && q0 > 1e-280 && R < 1e10 && x - lb > 0) {
-      const double R2 = R * R;
-      qn[0] = q0;           // lb
-      qn[1] = q0 * (R2 * R2);  // ub
-      qn[2] = q0 * R2;      // c
-      qn[3] = q0 * R;       // d
-      qn[4] = q0 * (R2 * R);   // e
-    }
-  }
-  // Shared series decision: ks(tt) increases and kl(tt) decreases with tt
-  // (pdf.pxi:36-47; ks only while its log argument stays below e^-1/2, hence
-  // the 0.5 test at the largest tt), so when the outermost t nodes (largest /
-  // smallest tt) take the same branch and K with both fp32 decisions clear of
-  // every threshold, all 5 nodes do. Otherwise each node decides itself.
-  // (The two end decisions also serve their own nodes, j = 0 and 1.)
-  Decision D0{0, 0}, D1{0, 0};
-  bool ok0 = false, ok1 = false, shared = false;
-  if (!WFPT_EXACT_MATH && x - ub > 0) {
-    const double a2 = a * a;
-    float args0, args1;
-    ok0 = decide32((x - lb) / a2, err, D0, args0);
-    ok1 = decide32((x - ub) / a2, err, D1, args1);
-    shared = ok0 && ok1 && args0 < 0.5f && D0.small == D1.small && D0.K == D1.K;
-  }
-  double f0 = 0.0, f1 = 0.0, f2 = 0.0, f3 = 0.0, f4 = 0.0;
-#pragma unroll 1
-  for (int j = 0; j < 5; ++j) {
-    const double tc = j == 0 ? lb : j == 1 ? ub : j == 2 ? c : j == 3 ? d : e;
-    const double qh = j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
-    const bool known = j == 0 ? ok0 : (j == 1 ? ok1 : shared);
-    const TNode T = tnode_setup(x - tc, v, sv, a, err, qh, known, j == 1 ? D1 : D0);
-    double y;
-    if (MODE == kAdaptTZ) {
-      y = level0_z(T, G, iZz, K.simps_err, K.n_sz, v, sv, a, slow) * iZt;
-#ifndef WFPT_EXP_NOEXIT
-      if (slow) return 0.0;
-#endif
-    } else {
-      y = tnode_pdf_sv(T, z, v, sv, a) * iZt;
-    }
-    if (j == 0) f0 = y;
-    else if (j == 1) f1 = y;
-    else if (j == 2) f2 = y;
-    else if (j == 3) f3 = y;
-    else f4 = y;
-  }
-  const double h = ub - lb;
-  const double S = (h / 6) * ((f0 + (4 * f2)) + f1);
-  const double Sl = (h / 12) * ((f0 + (4 * f3)) + f2);
-  const double Sr = (h / 12) * ((f2 + (4 * f4)) + f1);
-  const double S2 = Sl + Sr;
-  if (!(K.n_st <= 0 || fabs(S2 - S) <= 15 * K.simps_err)) slow = true;
-  return S2 + (S2 - S) / 15;
+  auto g = [&](double zc) -> double {
+    ++ne;
+    return tnode_pdf_sv(T, zc, v, sv, a) * iZz;
+  };
+  return adaptive_walk<RegStack<kInnerCap>>(g, lbz, ubz, K.simps_err, K.n_sz, flags, ne);
 }
 
-// evaluations of a trial that finished on the fast path (for W_trial counting)
-__host__ __device__ inline int fast_evals(int mode) {
-  return mode == kDirect ? 1 : (mode == kAdaptTZ ? 25 : 5);
+// Root interval of the adaptive tree: over t for kAdaptT / kAdaptTZ, over z
+// for kAdaptZ.
+template <int MODE>
+__device__ inline void tree_root(const Trial& tr, const Params& P, double& lb, double& ub) {
+  if (MODE == kAdaptZ) {
+    lb = tr.z - tr.sz / 2.;
+    ub = tr.z + tr.sz / 2.;
+  } else {
+    lb = P.t - tr.st / 2.;
+    ub = P.t + tr.st / 2.;
+  }
+}
+
+// Level-0 pass of one trial for an adaptive (or direct) MODE: the reference's
+// prologue + root aux node of every adaptive Simpson it runs (1, 5, 5 or 25
+// pdf_sv evaluations, + refinements of the z integrals in kAdaptTZ).
+//   kFinal: p is the trial density (0 for invalid parameters);
+//   kTree:  the root stop test asks for refinement; f[] = the root interval's
+//           values at lb, d, c, e, ub (continued by the level kernels);
+//   kExact: the value hinges on last-bit rounding (recomputed exactly);
+//   kFall:  continue on the per-lane walk.
+template <int MODE>
+__device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, double& p,
+                                  double (&f)[5], long long& ne, int& flags) {
+  const Trial tr = trial_setup(x0, P);
+  p = 0.0;
+  if (!tr.valid) return kFinal;
+  const double a = P.a, sv = P.sv, t = P.t, err = K.err;
+  const double x = tr.x, v = tr.v, z = tr.z;
+  if (MODE == kDirect) {
+    ne += 1;
+    p = pdf_sv(x - t, v, sv, a, z, err, flags);
+    if (flags & kFlagExact) return kExact;
+    return (p > kExactBelow || x - t <= 0) ? kFinal : kExact;
+  }
+  double lb, ub;
+  tree_root<MODE>(tr, P, lb, ub);
+  const double iw = 1.0 / (ub - lb);
+  if (MODE == kAdaptZ) {
+    const ZGrid G = zgrid_setup(lb, ub, v, sv, a);
+    const TNode T = tnode_setup(x - t, v, sv, a, err);
+    if (T.amb) return kExact;
+    tnode_pdf_sv_grid5(T, G, v, sv, a, f);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
+    ne += 5;
+  } else {
+    // t outer: kAdaptT (one evaluation per t node) or kAdaptTZ (a z integral
+    // per t node)
+    const double c = (ub + lb) / 2.;
+    const double d = (lb + c) / 2., e = (c + ub) / 2.;
+    const double lbz = z - tr.sz / 2., ubz = z + tr.sz / 2.;
+    const double iZz = (MODE == kAdaptTZ) ? 1.0 / (ubz - lbz) : 0.0;
+    unsigned repair = 0u;  // t nodes whose z integral needs refinement
+    {
+      ZGrid G;
+      if (MODE == kAdaptTZ) G = zgrid_setup(lbz, ubz, v, sv, a);
+      // large-time factor q = exp(-pi^2 (x - tc) / (2 a^2)) over the t grid:
+      // q(lb + j (ub - lb) / 4) = q(lb) R^j, R = exp(pi^2 (ub - lb) / (8 a^2))
+      // (values only; direct exps where the products leave the safe range)
+      double qn[5] = {-1.0, -1.0, -1.0, -1.0, -1.0};
+      {
+        const double a2 = a * a;
+        const double q0 = exp((-kPi2 * ((x - lb) / a2)) / 2.0);
+        const double R = exp((kPi2 * (ub - lb)) / (8.0 * a2));
+        if (q0 > 1e-280 && R < 1e10 && x - lb > 0) {
+          const double R2 = R * R;
+          qn[0] = q0;
+          qn[1] = q0 * R;
+          qn[2] = q0 * R2;
+          qn[3] = q0 * (R2 * R);
+          qn[4] = q0 * (R2 * R2);
+        }
+      }
+      // Shared series decision: ks(tt) increases and kl(tt) decreases with tt
+      // (pdf.pxi:36-47; ks only while its log argument stays below e^-1/2,
+      // hence the 0.5 test at the largest tt), so when the outermost t nodes
+      // (largest / smallest tt) take the same branch and K with both fp32
+      // decisions clear of every threshold, all 5 nodes do. Otherwise each
+      // node decides itself.
+      Decision D0{0, 0, 0}, D4{0, 0, 0};
+      bool ok0 = false, ok4 = false, shared = false;
+      if (x - ub > 0) {
+        const double a2 = a * a;
+        float args0, args4;
+        ok0 = decide32((x - lb) / a2, err, D0, args0);
+        ok4 = decide32((x - ub) / a2, err, D4, args4);
+        shared = ok0 && ok4 && args0 < 0.5f && D0.small == D4.small && D0.K == D4.K;
+      }
+#pragma unroll 1
+      for (int j = 0; j < 5; ++j) {
+        const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
+        const double qh = j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
+        const bool known = j == 0 ? ok0 : (j == 4 ? ok4 : shared);
+        const TNode T = tnode_setup(x - tc, v, sv, a, err, qh, known, j == 4 ? D4 : D0);
+        if (T.amb) return kExact;
+        double y;
+        if (MODE == kAdaptTZ) {
+          bool rep;
+          y = inner_root(T, G, iZz, v, sv, a, K, flags, ne, rep) * iw;
+          if (flags & kFlagExact) return kExact;
+          if (rep) repair |= 1u << j;
+        } else {
+          ne += 1;
+          y = tnode_pdf_sv(T, z, v, sv, a) * iw;
+        }
+        if (j == 0) f[0] = y;
+        else if (j == 1) f[1] = y;
+        else if (j == 2) f[2] = y;
+        else if (j == 3) f[3] = y;
+        else f[4] = y;
+      }
+    }
+    // z integrals whose root test asked for refinement, after the loop (few
+    // live registers here): the complete walk at that t node
+    if (MODE == kAdaptTZ) {
+      while (repair) {
+        const int j = __builtin_ctz(repair);
+        repair &= repair - 1u;
+        const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
+        const TNode T = tnode_setup(x - tc, v, sv, a, err);
+        ne -= 5;  // inner_full evaluates the root again
+        const double y = inner_full(T, lbz, ubz, iZz, v, sv, a, K, flags, ne) * iw;
+        if (flags & kFlagExact) return kExact;
+        if (flags & (kFlagFallback | kFlagErrors)) return kFall;
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+          if (k == j) f[k] = y;
+      }
+    }
+  }
+  const Simp s = simp5(ub - lb, f[0], f[1], f[2], f[3], f[4]);
+  const int bottom = (MODE == kAdaptZ) ? K.n_sz : K.n_st;
+  const bool refine = simpson_refine(s.S, s.S2, K.simps_err, bottom, flags);
+  if (flags & kFlagExact) return kExact;
+  if (refine) return kTree;
+  p = s.S2 + (s.S2 - s.S) / 15;
+  // structural zero: every evaluation point has x - t_node <= 0 (x == lb for t trees)
+  const bool structural = (MODE == kAdaptZ) ? x - t <= 0 : x - lb <= 0;
+  return (p > kExactBelow || structural) ? kFinal : kExact;
+}
+
+// Per-trial state of the tree function f(u) for the level kernels.
+template <int MODE>
+struct TreeFn {
+  Trial tr;
+  double lb, ub, iw;
+  double lbz, ubz, iZz;  // kAdaptTZ: the z range and 1 / (ub_z - lb_z)
+  ZGrid G;               // kAdaptTZ: root z grid
+  TNode T0;              // kAdaptZ: the trial's single t node
+  __device__ inline void setup(double x0, const Params& P, const Knobs& K) {
+    tr = trial_setup(x0, P);
+    tree_root<MODE>(tr, P, lb, ub);
+    iw = 1.0 / (ub - lb);
+    if (MODE == kAdaptTZ) {
+      lbz = tr.z - tr.sz / 2.;
+      ubz = tr.z + tr.sz / 2.;
+      iZz = 1.0 / (ubz - lbz);
+      G = zgrid_setup(lbz, ubz, tr.v, P.sv, P.a);
+    }
+    if (MODE == kAdaptZ) T0 = tnode_setup(tr.x - P.t, tr.v, P.sv, P.a, K.err);
+  }
+  // f(u) of the tree: pdf_sv(x - u, z) / st (T), pdf_sv(x - t, u) / sz (Z),
+  // [z integral at t node u] / st (TZ; root level only, repair = it needs
+  // refinement: then call full(u))
+  __device__ inline double operator()(double u, const Params& P, const Knobs& K, int& flags,
+                                      long long& ne, bool& repair) const {
+    repair = false;
+    if (MODE == kAdaptZ) {
+      if (T0.amb) flags |= kFlagExact;
+      ne += 1;
+      return tnode_pdf_sv(T0, u, tr.v, P.sv, P.a) * iw;
+    }
+    const TNode T = tnode_setup(tr.x - u, tr.v, P.sv, P.a, K.err);
+    if (T.amb) flags |= kFlagExact;
+    if (MODE == kAdaptT) {
+      ne += 1;
+      return tnode_pdf_sv(T, tr.z, tr.v, P.sv, P.a) * iw;
+    }
+    return inner_root(T, G, iZz, tr.v, P.sv, P.a, K, flags, ne, repair) * iw;
+  }
+  __device__ inline double full(double u, const Params& P, const Knobs& K, int& flags,
+                                long long& ne) const {
+    const TNode T = tnode_setup(tr.x - u, tr.v, P.sv, P.a, K.err);
+    ne -= 5;
+    return inner_full(T, lbz, ubz, iZz, tr.v, P.sv, P.a, K, flags, ne) * iw;
+  }
+};
+
+// Geometry of tree node (L, m) (m's bits = left/right turns from the root),
+// computed as the reference's recursion does: bounds by the midpoint
+// (ub + lb) / 2 of each parent, S = the parent's Sleft / Sright, err halved
+// per level. F(j) returns the stored value at dyadic point j.
+struct TreeNode {
+  double lb, ub, S, err;
+  int pos, W;
+};
+template <class FV>
+__device__ inline TreeNode tree_node(FV&& F, double lb0, double ub0, double err0, int L, int m) {
+  TreeNode n;
+  n.lb = lb0;
+  n.ub = ub0;
+  n.pos = 0;
+  n.W = kTreeW;
+  n.err = err0;
+  n.S = simp5(ub0 - lb0, F(0), 0.0, F(kTreeW / 2), 0.0, F(kTreeW)).S;
+  for (int l = 0; l < L; ++l) {
+    const int W = n.W;
+    const Simp s = simp5(n.ub - n.lb, F(n.pos), F(n.pos + W / 4), F(n.pos + W / 2),
+                         F(n.pos + 3 * W / 4), F(n.pos + W));
+    const double c = (n.ub + n.lb) / 2.;
+    if ((m >> (L - 1 - l)) & 1) {
+      n.lb = c;
+      n.S = s.Sr;
+      n.pos += W / 2;
+    } else {
+      n.ub = c;
+      n.S = s.Sl;
+    }
+    n.W = W / 2;
+    n.err = n.err / 2;
+  }
+  return n;
+}
+
+// The trial's integral from a completed tree: the reference's recursion
+// (leaf S2 + (S2 - S) / 15, internal left + right) re-walked over the stored
+// values; every stop test repeats the level kernels' arithmetic, so it takes
+// the same branch. Only called for trees within kBfDepth.
+template <class FV>
+__device__ inline double tree_value(FV&& F, double lb0, double ub0, double err0, int depth) {
+  struct Fr {
+    double lb, ub, S, err, left;
+    int pos, W;
+  };
+  Fr stk[kBfDepth > 0 ? kBfDepth : 1];
+  unsigned right_mask = 0u;
+  int sp = 0, bottom = depth;
+  double lb = lb0, ub = ub0, err = err0;
+  int pos = 0, W = kTreeW;
+  double S = simp5(ub0 - lb0, F(0), 0.0, F(kTreeW / 2), 0.0, F(kTreeW)).S;
+  for (;;) {
+    const Simp s = simp5(ub - lb, F(pos), F(pos + W / 4), F(pos + W / 2), F(pos + 3 * W / 4),
+                         F(pos + W));
+    int fl = 0;
+    const bool refine = simpson_refine(S, s.S2, err, bottom, fl);
+    if (refine && sp < kBfDepth) {
+      const double c = (ub + lb) / 2.;
+#pragma unroll
+      for (int k = 0; k < (kBfDepth > 0 ? kBfDepth : 1); ++k)
+        if (k == sp) stk[k] = Fr{c, ub, s.Sr, err / 2, 0.0, pos + W / 2, W / 2};
+      ++sp;
+      ub = c;
+      S = s.Sl;
+      err = err / 2;
+      W = W / 2;
+      bottom -= 1;
+      continue;
+    }
+    double val = s.S2 + (s.S2 - S) / 15;
+    bool done = false;
+    for (;;) {
+      if (sp == 0) {
+        done = true;
+        break;
+      }
+      const int top = sp - 1;
+      Fr fr = stk[0];
+#pragma unroll
+      for (int k = 1; k < (kBfDepth > 0 ? kBfDepth : 1); ++k)
+        if (k == top) fr = stk[k];
+      if (!((right_mask >> top) & 1u)) {
+#pragma unroll
+        for (int k = 0; k < (kBfDepth > 0 ? kBfDepth : 1); ++k)
+          if (k == top) stk[k].left = val;
+        right_mask |= 1u << top;
+        lb = fr.lb;
+        ub = fr.ub;
+        S = fr.S;
+        err = fr.err;
+        pos = fr.pos;
+        W = fr.W;
+        bottom = depth - sp;
+        break;
+      }
+      val = fr.left + val;
+      right_mask &= ~(1u << top);
+      --sp;
+    }
+    if (done) return val;
+  }
 }
 
 // P(hit upper boundary), pdf.pxi:67-72

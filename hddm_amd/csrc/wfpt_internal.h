@@ -4,51 +4,66 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <type_traits>
+
 #include "../../include/wfpt_amd.h"
 
 namespace wfpt {
 struct Params;
 struct Knobs;
 
+// Deferred-trial state of one adaptive call, slot-indexed (slot = chunk * 64 +
+// rank of the trial among its chunk's deferred trials; nslots = chunks * 64).
+struct Work {
+  unsigned char* wl;  // [nslots] lane of the trial in slot
+  int* wl_n;          // [chunks] #tree | #exact << 8 deferred trials of the chunk
+  int* rflag;         // [nslots] kFlag* of the trial in slot
+  double* F;          // [tree_points() * nslots] tree sample values (SoA)
+  int* rcnt;          // [nslots] pdf_sv evaluations so far (evaluation counting only)
+  uint32_t* tasks;    // [task_capacity(nslots)] tree-level task lists
+  int* ntask;         // [8] task counts per level (0 at rest)
+  int64_t nslots;
+};
+// task_offset / task_capacity / kTreePoints: wfpt_device.hpp
+
+// Error flags encoded as counts in one double that survives an RCCL sum:
+// (#ranks with a depth error) + kBudgetUnit * (#ranks with a budget error).
+constexpr double kBudgetUnit = 1048576.0;
+
 int stack_kind(const Knobs& K);
 int64_t blocks_for(int64_t n);
-// out_kind: 0 = block {sum, zeros}; 1 = per-trial density (logp => log); 2 = per-trial log p.
-// Adaptive modes run a level-0 fast pass then a slow pass over the deferred
-// trials: wl must hold blocks_for(n)*256 bytes and wl_n blocks_for(n) ints;
-// OUT_SUM then leaves partials_for(n) block partials in out/zeros.
-// fast_done (optional) is recorded right after the level-0 fast kernel.
-void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
-                   double* out, int* zeros, unsigned long long* evals, int* status, int logp,
-                   unsigned char* wl, int* wl_n, hipStream_t s,
-                   hipEvent_t fast_done = nullptr);
+// true: adaptive / direct family (level-0 pass + deferred pass); false: fixed
+// Simpson (one trial kernel).
+bool has_deferred_pass(const Params& P, const Knobs& K);
+// partials a sum leaves in out/zeros: one per 64-trial chunk (adaptive /
+// direct) or per 256-trial block (fixed Simpson)
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
-void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt);
-void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s);
-// Status bit the level-0 pass of a sum sets when it deferred trials (besides
-// the error bits 1 = Simpson depth, 2 = evaluation budget).
-constexpr int kStatusDeferred = 4;
-// The level-0 pass alone (adaptive modes; false, nothing launched, otherwise):
-// per-64-trial partials in part[0, ceil(n/64)) + worklists, and
-// kStatusDeferred in *status if any trial still needs the slow pass.
-bool launch_fast_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s,
-                      hipEvent_t fast_done);
-// res[0..2] (device) -> out[0..2] (mapped host), then out[3] = seq.
+
+// out_kind: 0 = partial {sum, zeros}; 1 = per-trial density (logp => log);
+// 2 = per-trial log p. part: kPassFast (level-0 pass, or the whole fixed
+// Simpson kernel) | kPassDeferred (tree levels + fold). fast_done (optional)
+// is recorded right after the level-0 / trial kernel.
+constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3;
+void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
+                   const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
+                   int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr);
+// out[0..3] = {sum of nb partials, #zero trials, encoded error flags, deferred
+// (any wl_n[0..nw) != 0; wl_n may be null)}, then out[4] = seq (a 64-bit
+// word) once they are visible; resets *status to 0.
+void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
+                     int* status, double* out, unsigned long long seq, hipStream_t s);
+// res[0..2] (device) -> out[0..2] (mapped host), out[3] = 0, then out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
-// out[0..2] = {sum, #zero trials, status flags & keep}, then out[3] = seq (as
-// a 64-bit word) once they are visible; resets *status to 0.
-void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
-                     unsigned long long seq, hipStream_t s, int keep = -1);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
 // two-pass fast path; d_idx / d_par hold up to n deferred trials, *n_defer
-// must be 0 on the stream), or -1 (mixed / fixed
-// Simpson: one generic per-trial kernel with a per-lane mode).
+// must be 0 on the stream), or -1 (mixed / fixed Simpson: one generic
+// per-trial kernel with a per-lane mode).
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
                   int* n_defer, unsigned long long* evals, int* status, hipStream_t s);
 // res (device, n_nodes) per-node sums; then out (mapped host): [0, n_nodes)
-// the sums, [n_nodes] status flags, [n_nodes + 1] the 64-bit completion word.
+// the sums, [n_nodes] encoded error flags, [n_nodes + 1] the completion word.
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s);
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,

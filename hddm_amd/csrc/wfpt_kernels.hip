@@ -1,14 +1,24 @@
 // wfpt_kernels.hip — gfx950 kernels of the WFPT likelihood engine.
 //
-//   trial_kernel<MODE, STK, COUNT, OUT>   one trial per lane: full_pdf, the
-//       outlier mixture (wfpt.pyx:69-70) and either the per-block
-//       {sum log p, #zeros} (OUT_SUM, fused wave/LDS tree reduction) or the
-//       per-trial density / log density (OUT_ARRAY, pdf_array), or per-trial
-//       log p for the segmented per-node reduction (OUT_LOGP).
-//   finalize_kernel       deterministic second pass over block partials.
-//   segment_sum_kernel    per-node sums (one wave per node).
-//   multi_kernel          per-trial parameters (wiener_like_multi).
-// No float atomics on any likelihood value: every sum is a fixed-order tree.
+// Adaptive / direct integration families (the HDDM case), one call:
+//   fast_kernel<MODE>     level-0 pass, one 64-trial chunk per wave: trials
+//                         whose root Simpson tests pass finish here (mixture,
+//                         log, per-chunk partial); the others are compacted per
+//                         chunk into tree records (refinement) or exact records
+//   gather_kernel         level-1 task list from the per-chunk counts
+//   level_kernel<MODE,L>  tree level L breadth-first over all deferred trials:
+//                         one task = one interval (2 new sample points + its
+//                         stop test), refined intervals push their children
+//   fold_kernel<MODE>     per chunk: the deferred trials' densities (tree
+//                         re-walk, exact path, per-lane fallback), mixture and
+//                         log, added to the chunk's partial in lane order
+//   finalize_kernel       fixed-order sum of the chunk partials -> mapped slot
+// The per-chunk partial of a chunk is the same value whether or not the call
+// ran the deferred kernels (a chunk without deferred trials is never touched),
+// so a likelihood is bitwise reproducible across call sequences. No float
+// atomics on any likelihood value.
+// Fixed Simpson (use_adaptive = 0): trial_kernel. Per-node and per-trial
+// parameter variants: node_*_kernel, multi_kernel.
 #include "wfpt_device.hpp"
 #include "wfpt_internal.h"
 
@@ -27,8 +37,7 @@ static inline int64_t fast_blocks(int64_t n) { return (n + kFastBlock - 1) / kFa
 
 // Minimum waves per SIMD requested for the level-0 fast kernels (0 = let the
 // compiler choose): WFPT_FAST_WAVES for the 1-D / direct modes,
-// WFPT_FAST_WAVES_TZ for the 2-D mode (5-wide z evaluation: 199 VGPRs, 2 waves
-// spill-free; 3 waves spill 36). Chosen by tools/ab_variants.py on MI355X.
+// WFPT_FAST_WAVES_TZ for the 2-D mode. Chosen by tools/ab_variants.py.
 #ifndef WFPT_FAST_WAVES
 #define WFPT_FAST_WAVES 3
 #endif
@@ -39,17 +48,16 @@ template <int MODE>
 struct FastWaves {
   static constexpr int value = MODE == kAdaptTZ ? WFPT_FAST_WAVES_TZ : WFPT_FAST_WAVES;
 };
-// Minimum waves per SIMD of the general (recursive) kernels (slow pass, generic
-// per-trial / per-node / per-trial-parameter kernels):
-// left free their register use reaches 255 VGPRs + 2 AGPRs, one past the
-// 2-wave budget (1 wave / SIMD); 2 keeps them at 256 with a little more scratch.
+// Minimum waves per SIMD of the general (per-lane walk) kernels.
 #ifndef WFPT_SLOW_WAVES
 #define WFPT_SLOW_WAVES 2
 #endif
-// Blocks (one wave each) of the deferred-trial pass: one per SIMD slot it can
-// occupy (256 CUs x 4 SIMDs x WFPT_SLOW_WAVES).
-#ifndef WFPT_SLOW_GRID
-#define WFPT_SLOW_GRID 2048
+// Blocks of the grid-stride deferred-trial kernels (level and fold).
+#ifndef WFPT_LEVEL_GRID
+#define WFPT_LEVEL_GRID 2048
+#endif
+#ifndef WFPT_FOLD_GRID
+#define WFPT_FOLD_GRID 2048
 #endif
 
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
@@ -64,6 +72,7 @@ __device__ inline long long wave_sum_ll(long long v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+__device__ inline unsigned long long lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
 
 // Block (256 lanes = 4 waves) reduction of (sum, zeros, evals); lane 0 returns.
 template <bool COUNT>
@@ -94,47 +103,263 @@ struct TrialArgs {
   Params P;
   Knobs K;
   double wp_outlier;      // w_outlier * p_outlier
-  double* out;            // OUT_SUM: block sums; OUT_ARRAY/OUT_LOGP: per trial
-  int* zeros;             // OUT_SUM: block zero counts
+  double* out;            // OUT_SUM: chunk / block partial sums; OUT_ARRAY/OUT_LOGP: per trial
+  int* zeros;             // OUT_SUM: chunk / block zero counts
   unsigned long long* evals;
-  int* status;            // set to 1 if a trial overflowed the Simpson stack
+  int* status;            // error flags (kFlagDepth | kFlagBudget)
   int logp;               // OUT_ARRAY: return log density
 };
 
-template <int STK>
-struct StackOf;
-template <>
-struct StackOf<0> {
-  using type = RegStack<2>;
-};
-template <>
-struct StackOf<1> {
-  using type = RegStack<4>;
-};
-template <>
-struct StackOf<2> {
-  using type = MemStack<WFPT_MAX_DEPTH>;
-};
+// Trial output of a settled density p (wfpt.pyx:44 / :70).
+template <int OUT>
+__device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp, int& zero) {
+  if (OUT == OUT_ARRAY) {
+    p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
+    A.out[i] = A.logp ? log(p) : p;
+  } else {
+    p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
+    if (p == 0) zero = 1;
+    else lp = log(p);
+    if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+  }
+}
 
-template <int MODE, int STK, bool COUNT, int OUT>
+// ---------------------------------------------------------------------------
+// Level-0 pass. One wave = one chunk of 64 consecutive trials c*64 + lane.
+// Deferred trials of chunk c take slots c*64 + k (k = their rank among the
+// chunk's tree trials, then among its exact trials), so the deferred state is
+// slot-indexed without any atomic.
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void fast_kernel(TrialArgs A, Work W) {
+  // ascending |rt| in dispatch order: the costlier short-RT chunks start first
+  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t c = i >> 6;
+  double p = 0.0, f[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  long long ne = 0;
+  int flags = 0, oc = kFinal;
+  if (i < A.n) oc = fast_level0<MODE>(A.x[i], A.P, A.K, p, f, ne, flags);
+  double lp = 0.0;
+  int zero = 0;
+  if (i < A.n && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
+  // tree records first, then exact / per-lane-walk records
+  const unsigned long long bt = __ballot(oc == kTree), be = __ballot(oc >= kExact);
+  const int nt = __popcll(bt);
+  if (oc != kFinal) {
+    const int k = oc == kTree ? __popcll(bt & lanemask_lt(lane))
+                              : nt + __popcll(be & lanemask_lt(lane));
+    const int64_t slot = c * 64 + k;
+    W.wl[slot] = (unsigned char)lane;
+    W.rflag[slot] = oc == kExact ? (int)kFlagExact : (oc == kFall ? (int)kFlagFallback : 0);
+    if (oc == kTree) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) W.F[(int64_t)(j * (kTreeW / 4)) * W.nslots + slot] = f[j];
+    }
+    if (COUNT) W.rcnt[slot] = oc == kTree ? (int)ne : 0;
+  }
+  if (lane == 0) W.wl_n[c] = nt | (__popcll(be) << 8);
+  if (OUT == OUT_SUM) {
+    lp = wave_sum(lp);
+    const int zs = __popcll(__ballot(zero != 0));
+    if (lane == 0) {
+      A.out[c] = lp;
+      A.zeros[c] = zs;
+    }
+  }
+  if (COUNT) {
+    const long long nf = wave_sum_ll(oc == kFinal ? ne : 0);
+    if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
+  }
+}
+
+// Level-1 tasks (both halves of every tree record's root interval) from the
+// per-chunk tree counts: one wave per 64 chunks, one atomic per wave.
+__global__ __launch_bounds__(256) void gather_kernel(const int* wl_n, int64_t nw, Work W) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int nt = c < nw ? (wl_n[c] & 255) : 0;
+  // wave inclusive prefix of 2 * nt
+  int v = 2 * nt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  const int tot = __shfl(v, 63, 64);
+  int base = 0;
+  if (lane == 63 && tot) base = atomicAdd(&W.ntask[1], tot);
+  base = __shfl(base, 63, 64);
+  uint32_t* t1 = W.tasks + task_offset(1, W.nslots);
+  int at = base + v - 2 * nt;
+  for (int k = 0; k < nt; ++k) {
+    const uint32_t slot = (uint32_t)(c * 64 + k);
+    t1[at++] = slot << kBfDepth;
+    t1[at++] = (slot << kBfDepth) | 1u;
+  }
+}
+
+// Tree level L (1..kBfDepth) breadth-first: one lane per interval of the
+// level. Evaluates f at the interval's d and e (the reference's
+// adaptiveSimpsonsAux evaluations, integrate.pxi:94-104 / 161-169), stores
+// them in the record, runs the stop test and pushes both halves to level L+1
+// when it asks for refinement (past kBfDepth: the record continues on the
+// per-lane walk in fold_kernel). A near-tie marks the record exact; its other
+// tasks then stop.
+template <int MODE, int L, bool COUNT>
+__global__ __launch_bounds__(256) void level_kernel(TrialArgs A, Work W, int depth) {
+  const int nt = W.ntask[L];
+  const uint32_t* tl = W.tasks + task_offset(L, W.nslots);
+  uint32_t* next = L < kBfDepth ? W.tasks + task_offset(L + 1, W.nslots) : nullptr;
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); base < nt; base += stride) {
+    const int64_t t = base + lane;
+    bool push = false;
+    int64_t slot = 0;
+    int m = 0;
+    if (t < nt) {
+      const uint32_t e = tl[t];
+      slot = e >> kBfDepth;
+      m = (int)(e & ((1u << kBfDepth) - 1u));
+      if (!(W.rflag[slot] & (kFlagExact | kFlagFallback))) {
+        const int64_t i = (slot >> 6) * 64 + W.wl[slot];
+        TreeFn<MODE> fn;
+        fn.setup(A.x[i], A.P, A.K);
+        const int64_t ns = W.nslots;
+        double* F = W.F;
+        auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
+        const TreeNode nd = tree_node(FV, fn.lb, fn.ub, A.K.simps_err, L, m);
+        const double c = (nd.ub + nd.lb) / 2.;
+        const double d = (nd.lb + c) / 2., ee = (c + nd.ub) / 2.;
+        int fl = 0;
+        long long ne = 0;
+        bool rd = false, re = false;
+        double fd = fn(d, A.P, A.K, fl, ne, rd);
+        double fe = 0.0;
+        if (!(fl & kFlagExact)) fe = fn(ee, A.P, A.K, fl, ne, re);
+        // z integrals that need refinement (kAdaptTZ), after both roots
+        if (rd && !(fl & kFlagExact)) fd = fn.full(d, A.P, A.K, fl, ne);
+        if (re && !(fl & kFlagExact)) fe = fn.full(ee, A.P, A.K, fl, ne);
+        if (fl & (kFlagFallback | kFlagErrors)) {
+          atomicOr(&W.rflag[slot], (int)kFlagFallback);
+          fl &= ~kFlagErrors;
+        } else if (!(fl & kFlagExact)) {
+          F[(int64_t)(nd.pos + nd.W / 4) * ns + slot] = fd;
+          F[(int64_t)(nd.pos + 3 * nd.W / 4) * ns + slot] = fe;
+          const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), fd, FV(nd.pos + nd.W / 2), fe,
+                               FV(nd.pos + nd.W));
+          const bool refine = simpson_refine(nd.S, s.S2, nd.err, depth - L, fl);
+          if (!(fl & kFlagExact) && refine) {
+            if (L < kBfDepth) push = true;
+            else atomicOr(&W.rflag[slot], (int)kFlagFallback);
+          }
+        }
+        if (fl & kFlagExact) atomicOr(&W.rflag[slot], (int)kFlagExact);
+        if (fl & kFlagErrors) atomicOr(A.status, fl & kFlagErrors);
+        if (COUNT) atomicAdd(&W.rcnt[slot], (int)ne);
+      }
+    }
+    if (L < kBfDepth) {
+      const unsigned long long b = __ballot(push);
+      if (b) {
+        int nb = 0;
+        if (lane == 0) nb = atomicAdd(&W.ntask[L + 1], 2 * __popcll(b));
+        nb = __shfl(nb, 0, 64);
+        if (push) {
+          const int at = nb + 2 * __popcll(b & lanemask_lt(lane));
+          next[at] = ((uint32_t)slot << kBfDepth) | (uint32_t)(2 * m);
+          next[at + 1] = ((uint32_t)slot << kBfDepth) | (uint32_t)(2 * m + 1);
+        }
+      }
+    }
+  }
+}
+
+// Settles every deferred trial and folds it into its chunk: block g walks
+// chunks g, g + G, ... (64 chunk counts per parallel load); a chunk's deferred
+// trials run on its first lanes: tree records re-walk their completed tree,
+// exact records take the exact path, deeper trees the per-lane walk. OUT_SUM:
+// chunk partial += wave sum of the deferred log densities (fixed lane order).
+// Last kernel of the deferred sequence: resets the level counters.
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw,
+                                                                 int depth) {
+  const int lane = threadIdx.x;
+  const int64_t G = gridDim.x;
+  long long ne = 0;
+  int errf = 0;
+  for (int64_t b0 = blockIdx.x; b0 < nw; b0 += 64 * G) {
+    const int64_t myc = b0 + lane * G;
+    const int mycnt = myc < nw ? W.wl_n[myc] : 0;
+    unsigned long long work = __ballot(mycnt != 0);
+    while (work) {
+      const int j = __ffsll((long long)work) - 1;
+      work &= work - 1;
+      const int wn = __shfl(mycnt, j, 64);
+      const int ntot = (wn & 255) + (wn >> 8);
+      const int64_t c = b0 + (int64_t)j * G;
+      double lp = 0.0;
+      int zero = 0;
+      if (lane < ntot) {
+        const int64_t slot = c * 64 + lane;
+        const int64_t i = c * 64 + W.wl[slot];
+        const double x = A.x[i];
+        const int fl = W.rflag[slot];
+        long long n1 = 0;
+        double p;
+        if (fl & kFlagExact) {
+          p = exact_pdf(x, A.P, A.K, &n1, &errf);
+        } else if (fl & kFlagFallback) {
+          p = fallback_pdf<MODE>(x, A.P, A.K, &n1, &errf);
+        } else {
+          const Trial tr = trial_setup(x, A.P);
+          double lb, ub;
+          tree_root<MODE>(tr, A.P, lb, ub);
+          const int64_t ns = W.nslots;
+          const double* F = W.F;
+          p = tree_value([&](int q) -> double { return F[(int64_t)q * ns + slot]; }, lb, ub,
+                         A.K.simps_err, depth);
+          if (COUNT) n1 = W.rcnt[slot];
+          const bool structural = (MODE == kAdaptZ) ? tr.x - A.P.t <= 0 : tr.x - lb <= 0;
+          p = settle(p, x, A.P, A.K, structural, n1, errf);
+        }
+        ne += n1;
+        emit<OUT>(A, i, p, lp, zero);
+      }
+      if (OUT == OUT_SUM) {
+        lp = wave_sum(lp);
+        const int zs = __popcll(__ballot(zero != 0));
+        if (lane == 0) {
+          A.out[c] = A.out[c] + lp;
+          A.zeros[c] = A.zeros[c] + zs;
+        }
+      }
+    }
+  }
+  if (errf & kFlagErrors) atomicOr(A.status, errf & kFlagErrors);
+  if (COUNT) {
+    ne = wave_sum_ll(ne);
+    if (lane == 0) atomicAdd(A.evals, (unsigned long long)ne);
+  }
+  if (blockIdx.x == 0 && lane <= kBfDepth) W.ntask[lane] = 0;
+}
+
+// ---------------------------------------------------------------------------
+// Fixed composite Simpson (use_adaptive = 0): one trial per lane, full_pdf +
+// settle, per-block {sum, zeros} (OUT_SUM) or per-trial outputs.
+template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArgs A) {
-  using Stack = typename StackOf<STK>::type;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   long long ne = 0;
   double lp = 0.0;
-  int zero = 0, ovf = 0;
+  int zero = 0, flags = 0;
   if (i < A.n) {
-    double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
-    if (ovf) atomicOr(A.status, ovf);
-    if (OUT == OUT_ARRAY) {
-      p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
-      A.out[i] = A.logp ? log(p) : p;
-    } else {
-      p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
-      if (p == 0) zero = 1;
-      else lp = log(p);
-      if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
-    }
+    const double x = A.x[i];
+    double p = full_pdf<MODE, RegStack<2>>(x, A.P, A.K, ne, flags);
+    p = settle(p, x, A.P, A.K, !trial_setup(x, A.P).valid, ne, flags);
+    if (flags & kFlagErrors) atomicOr(A.status, flags & kFlagErrors);
+    emit<OUT>(A, i, p, lp, zero);
   }
   if (OUT == OUT_SUM || COUNT) {
     block_reduce<COUNT>(lp, zero, ne);
@@ -148,173 +373,20 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
   }
 }
 
-// Level-0 fast pass (MODE in kDirect..kAdaptTZ). Trials whose root Simpson
-// tests all pass are finished here; the others are compacted per WAVE into
-// `wl` (lane ids, one byte each, 64 slots per wave) and counted in
-// `wl_n[wave]` for slow_kernel. Barrier-free: every wave writes its own
-// partial sum / zero count (A.out[wave], A.zeros[wave]) and worklist, so a
-// wave that finishes early never waits for its block.
-//
-// fast_chunk: one 64-trial chunk of the level-0 pass for the calling wave: trial
-// i = c*64 + lane with RT xi (ignored when i >= n). Writes the chunk's
-// worklist, partial sum and zero count; returns the wave-reduced partial (lp,
-// zs) and the deferred count.
-template <int MODE, bool COUNT, int OUT>
-__device__ __forceinline__ void fast_chunk(const TrialArgs& A, unsigned char* wl, int* wl_n,
-                                           int64_t c, int lane, double xi, double& lp_out,
-                                           int& zs_out, int& nslow_out) {
-  const int64_t i = c * 64 + lane;
-  const int64_t wave = c;
-  long long ne = 0;
-  double lp = 0.0;
-  int zero = 0;
-  bool slow = false;
-  if (i < A.n) {
-    int valid = 0;
-    double p = fast_pdf<MODE>(xi, A.P, A.K, slow, valid);
-    if (!slow) {
-      if (COUNT && valid) ne = fast_evals(MODE);
-      if (OUT == OUT_ARRAY) {
-        p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
-        A.out[i] = A.logp ? log(p) : p;
-      } else {
-        p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
-        if (p == 0) zero = 1;
-        else lp = log(p);
-        if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
-      }
-    }
-  }
-  int nslow = 0;
-  if (MODE != kDirect) {
-    const unsigned long long b = __ballot(slow);
-    if (slow) wl[wave * 64 + __popcll(b & ((1ull << lane) - 1ull))] = (unsigned char)lane;
-    nslow = __popcll(b);
-    if (lane == 0) wl_n[wave] = nslow;
-    // tells the host this call deferred trials (the fast-only call sequence
-    // of wfpt_capi.cpp relies on it)
-    if (OUT == OUT_SUM && lane == 0 && nslow) atomicOr(A.status, kStatusDeferred);
-  }
-  int zs = 0;
-  if (OUT == OUT_SUM || COUNT) {
-    lp = wave_sum(lp);
-    zs = __popcll(__ballot(zero != 0));
-    if (COUNT) ne = wave_sum_ll(ne);
-    if (lane == 0) {
-      if (OUT == OUT_SUM) {
-        A.out[wave] = lp;
-        A.zeros[wave] = zs;
-      }
-      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
-    }
-  }
-  lp_out = lp;
-  zs_out = zs;
-  nslow_out = nslow;
-}
-
-template <int MODE, bool COUNT, int OUT>
-__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void fast_kernel(TrialArgs A, unsigned char* wl, int* wl_n) {
-  // ascending |rt| in dispatch order: the costlier short-RT chunks start first
-  // (dispatching largest |rt| first measured 3% slower)
-  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  double lp;
-  int zs, nslow;
-  fast_chunk<MODE, COUNT, OUT>(A, wl, wl_n, i >> 6, lane, i < A.n ? A.x[i] : 0.0, lp, zs, nslow);
-}
-
-// General pass over the trials the fast pass deferred. The fast pass leaves
-// one worklist and one partial per 64 trials (nl lists); this
-// one-wave-per-block kernel runs on a bounded grid of kSlowGrid blocks — one
-// wave per SIMD, which is all its register footprint (the general recursion,
-// ~255 VGPRs) lets reside anyway — and block g walks lists g, g + G, ...,
-// running the wl_n[b] deferred trials of list b on its first lanes (full
-// adaptive quadrature, reference recursion order). An empty list costs one
-// load, so a workload with (almost) nothing deferred pays one short
-// launch. For OUT_SUM the block also folds the fast partials of its lists
-// into its own (lane j takes list g + jG of each 64-list chunk) and writes
-// A.out[nb + g] / A.zeros[nb + g]: finalize then sums G values. Fixed order
-// for a given n.
-constexpr int64_t kSlowGrid = WFPT_SLOW_GRID;
-
-template <int MODE, int STK, bool COUNT, int OUT>
-__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void slow_kernel(TrialArgs A, const unsigned char* wl,
-                                                  const int* wl_n, int64_t nl, int64_t nb) {
-  using Stack = typename StackOf<STK>::type;
-  long long ne = 0;
-  double lp = 0.0;
-  long long zc = 0;
-  int ovf = 0;
-  const int lane = threadIdx.x;
-  const int64_t G = gridDim.x;
-  // chunks of 64 lists (g + j G, j = 0..63): one parallel load of their
-  // counts and fast partials, then only the non-empty lists are walked
-  for (int64_t b0 = blockIdx.x; b0 < nl; b0 += 64 * G) {
-    const int64_t myb = b0 + lane * G;
-    int mycnt = 0;
-    if (myb < nl) {
-      mycnt = wl_n[myb];
-      if (OUT == OUT_SUM) {
-        lp += A.out[myb];
-        zc += A.zeros[myb];
-      }
-    }
-    // one list at a time on its first lanes: the trials of a list are
-    // neighbours in |rt| and refine alike (packing the 64 lists' trials into
-    // full waves mixes distant |rt| and measured 3% slower on the stress set)
-    unsigned long long work = __ballot(mycnt > 0);
-    while (work) {
-      const int j = __ffsll((long long)work) - 1;
-      work &= work - 1;
-      const int cnt = __shfl(mycnt, j, 64);
-      const int64_t b = b0 + (int64_t)j * G;
-      if (lane >= cnt) continue;
-      const int64_t i = b * 64 + wl[b * 64 + lane];
-      double p = full_pdf<MODE, Stack, COUNT>(A.x[i], A.P, A.K, ne, ovf);
-      if (OUT == OUT_ARRAY) {
-        p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);
-        A.out[i] = A.logp ? log(p) : p;
-      } else {
-        p = p * (1 - A.P.p_outlier) + A.wp_outlier;
-        const bool z = p == 0;
-        double l = 0.0;
-        if (z) zc += 1;
-        else l = log(p);
-        lp += l;
-        if (OUT == OUT_LOGP) A.out[i] = z ? -INFINITY : l;
-      }
-    }
-  }
-  if (ovf) atomicOr(A.status, ovf);
-  if (OUT == OUT_SUM || COUNT) {
-    lp = wave_sum(lp);
-    zc = wave_sum_ll(zc);
-    if (COUNT) ne = wave_sum_ll(ne);
-    if (threadIdx.x == 0) {
-      if (OUT == OUT_SUM) {
-        A.out[nb + blockIdx.x] = lp;
-        A.zeros[nb + blockIdx.x] = (int)zc;
-      }
-      if (COUNT) atomicAdd(A.evals, (unsigned long long)ne);
-    }
-  }
-}
-
-__host__ __device__ inline int64_t slow_grid(int64_t nl) { return nl < kSlowGrid ? nl : kSlowGrid; }
-
-// out[0] = sum of partials, out[1] = number of zero trials, out[2] = the
-// call's status flags (as doubles); the device status word is reset to 0 for
-// the next call. `out` may be mapped pinned host memory: the 24-byte result
-// then reaches the host with the kernel, without a copy. Fixed summation
-// order for a given nb (4 independent accumulators per thread keep 4 loads
-// in flight).
+// out[0] = sum of nb partials, out[1] = number of zero trials, out[2] = error
+// flags encoded as counts that survive a sum over ranks (depth + 2^20 budget),
+// out[3] = 1 if the level-0 pass deferred trials (wl_n non-null: any chunk
+// count), then the 64-bit completion word out[4] once they are visible. `out`
+// may be mapped pinned host memory. Resets the device status word. Fixed
+// summation order for a given nb (4 accumulators per thread keep 4 loads in
+// flight).
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
-                                                        int64_t nb, int* status, double* out,
-                                                        unsigned long long seq, int keep) {
+                                                        int64_t nb, const int* wl_n, int64_t nw,
+                                                        int* status, double* out,
+                                                        unsigned long long seq) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
+  __shared__ int sd[16];
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   long long z = 0;
   int64_t b = threadIdx.x;
@@ -329,45 +401,54 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     s0 += part[b];
     z += zeros[b];
   }
+  int def = 0;
+  if (wl_n)
+    for (int64_t c = threadIdx.x; c < nw; c += 1024) def |= wl_n[c];
   double s = (s0 + s1) + (s2 + s3);
   s = wave_sum(s);
   z = wave_sum_ll(z);
+  const bool anyd = __ballot(def != 0) != 0ull;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) {
     ss[w] = s;
     sz[w] = z;
+    sd[w] = anyd;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     double t = 0.0;
     long long zz = 0;
+    int dd = 0;
     for (int k = 0; k < 16; ++k) {
       t += ss[k];
       zz += sz[k];
+      dd |= sd[k];
     }
     const int st = *status;
     *status = 0;
     out[0] = t;
     out[1] = (double)zz;
-    out[2] = (double)(st & keep);
+    out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+    out[3] = (double)dd;
     __threadfence_system();
     // completion word, written after the results are visible: the host may
     // poll it instead of waiting on the stream
-    reinterpret_cast<volatile unsigned long long*>(out)[3] = seq;
+    reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
     __threadfence_system();
   }
 }
 
-// Copies a device result {sum, zeros, status} (after the RCCL all-reduce) to
-// the mapped host slot, then writes the completion word (as finalize_kernel).
+// Copies a device result {sum, zeros, errors} (after the RCCL all-reduce) to
+// the mapped host slot, then writes the completion word.
 __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* out,
                                                      unsigned long long seq) {
   if (threadIdx.x == 0) {
     out[0] = res[0];
     out[1] = res[1];
     out[2] = res[2];
+    out[3] = 0.0;
     __threadfence_system();
-    reinterpret_cast<volatile unsigned long long*>(out)[3] = seq;
+    reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
     __threadfence_system();
   }
 }
@@ -397,8 +478,8 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, cons
 }
 
 // One block: copies the per-node sums to the mapped host slot, then the
-// call's status flags (out[n]) and, once all of it is visible, the 64-bit
-// completion word (out[n + 1]); resets the device status word.
+// call's encoded error flags (out[n]) and, once all of it is visible, the
+// 64-bit completion word (out[n + 1]); resets the device status word.
 __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, int32_t n,
                                                             int* status, double* out,
                                                             unsigned long long seq) {
@@ -406,13 +487,15 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {
-    out[n] = (double)atomicExch(status, 0);
+    const int st = atomicExch(status, 0);
+    out[n] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
     __threadfence_system();
     reinterpret_cast<volatile unsigned long long*>(out + n + 1)[0] = seq;
     __threadfence_system();
   }
 }
 
+// ---------------------------------------------------------------------------
 // Per-node parameters (wfpt_wiener_like_nodes): trials of node j use P[j].
 // The dataset is grouped by node, so a 256-trial block spans a short run of
 // node ids; their parameter rows (P is the mapped pinned table the host
@@ -421,11 +504,23 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
 // between) read the table directly.
 constexpr int kStageRows = 256;
 
+template <int STK>
+struct StackOf {
+  using type = typename std::conditional<
+      STK == 0, RegStack<2>,
+      typename std::conditional<STK == 1, RegStack<4>, MemStack<WFPT_MAX_DEPTH>>::type>::type;
+};
+
+__device__ inline double node_logp(double p, const Params& Q, const Knobs& K) {
+  const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);  // wfpt.pyx:63-64 per node
+  p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
+  return (!ok || p == 0) ? -INFINITY : log(p);
+}
+
 template <int STK, bool COUNT>
-__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(const double* x, const int32_t* node,
-                                                      int64_t n, const Params* P, Knobs K,
-                                                      double* lp, unsigned long long* evals,
-                                                      int* status) {
+__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(
+    const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
+    unsigned long long* evals, int* status) {
   using Stack = typename StackOf<STK>::type;
   __shared__ Params rows[kStageRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
@@ -441,18 +536,14 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(const dou
   }
   __syncthreads();
   long long ne = 0;
-  double out = 0.0;
-  int zero = 0, ovf = 0;
+  int zero = 0, flags = 0;
   if (i < n) {
     const int nj = node[i];
     const Params Q = staged ? rows[nj - first] : P[nj];
-    double p = full_pdf<kRuntime, Stack, COUNT>(x[i], Q, K, ne, ovf);
-    if (ovf) atomicOr(status, ovf);
-    const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);
-    p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
-    if (!ok || p == 0) zero = 1;
-    else out = log(p);
-    lp[i] = zero ? -INFINITY : out;
+    double p = full_pdf<kRuntime, Stack>(x[i], Q, K, ne, flags);
+    p = settle(p, x[i], Q, K, !trial_setup(x[i], Q).valid, ne, flags);
+    if (flags & kFlagErrors) atomicOr(status, flags & kFlagErrors);
+    lp[i] = node_logp(p, Q, K);
   }
   if (COUNT) {
     double d = 0.0;
@@ -463,22 +554,16 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(const dou
 
 // Two-pass per-node path (used when every node's parameters select the same
 // integration family, the usual HDDM case: sv/sz/st are group-level):
-// node_fast_kernel is fast_kernel with the node's parameter row (staged in
-// LDS as in node_kernel) and per-trial log p out; a trial that needs
-// refinement is appended — index and parameter row — to a dense deferred
-// list (wave-aggregated atomic; the order does not matter, outputs are per
-// trial), which node_slow_kernel runs 64 trials per wave.
-__device__ inline double node_logp(double p, const Params& Q, const Knobs& K) {
-  const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);  // wfpt.pyx:63-64 per node
-  p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
-  return (!ok || p == 0) ? -INFINITY : log(p);
-}
-
+// node_fast_kernel is the level-0 pass with the node's parameter row (staged
+// in LDS as in node_kernel) and per-trial log p out; a trial that needs
+// refinement or the exact path is appended — index and parameter row — to a
+// dense deferred list (wave-aggregated atomic; outputs are per trial, so the
+// order does not matter), which node_slow_kernel runs 64 trials per wave.
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
                       double* lp, int64_t* d_idx, Params* d_par, int* n_defer,
-                      unsigned long long* evals) {
+                      unsigned long long* evals, int* status) {
   __shared__ Params rows[kStageRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
   const int64_t i = i0 + threadIdx.x;
@@ -494,53 +579,55 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   }
   __syncthreads();
   long long ne = 0;
-  bool slow = false;
+  bool defer = false;
   Params Q;
   if (i < n) {
     const int nj = node[i];
     Q = staged ? rows[nj - first] : P[nj];
-    int valid = 0;
-    const double p = fast_pdf<MODE>(x[i], Q, K, slow, valid);
-    if (!slow) {
-      if (COUNT && valid) ne = fast_evals(MODE);
-      lp[i] = node_logp(p, Q, K);
-    }
+    double p, f[5];
+    int flags = 0;
+    const int oc = fast_level0<MODE>(x[i], Q, K, p, f, ne, flags);
+    if (oc == kFinal) lp[i] = node_logp(p, Q, K);
+    else defer = true;
   }
-  if (MODE != kDirect) {
-    const unsigned long long b = __ballot(slow);
-    if (b) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
-      base = __shfl(base, 0, 64);
-      if (slow) {
-        const int k = base + __popcll(b & ((1ull << lane) - 1ull));
-        d_idx[k] = i;
-        d_par[k] = Q;
-      }
+  const unsigned long long b = __ballot(defer);
+  if (b) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
+    base = __shfl(base, 0, 64);
+    if (defer) {
+      const int k = base + __popcll(b & lanemask_lt(lane));
+      d_idx[k] = i;
+      d_par[k] = Q;
     }
   }
   if (COUNT) {
-    ne = wave_sum_ll(ne);
+    ne = wave_sum_ll(defer ? 0 : ne);
     if (lane == 0) atomicAdd(evals, (unsigned long long)ne);
   }
 }
 
 template <int MODE, int STK, bool COUNT>
-__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(const double* x, Knobs K, double* lp,
-                                                       const int64_t* d_idx, const Params* d_par,
-                                                       const int* n_defer,
-                                                       unsigned long long* evals, int* status) {
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(
+    const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
+    const int* n_defer, unsigned long long* evals, int* status) {
   using Stack = typename StackOf<STK>::type;
   const int nd = *n_defer;
   long long ne = 0;
-  int ovf = 0;
+  int flags = 0;
   for (int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x; k < nd; k += (int64_t)gridDim.x * 64) {
     const int64_t i = d_idx[k];
     const Params Q = d_par[k];
-    const double p = full_pdf<MODE, Stack, COUNT>(x[i], Q, K, ne, ovf);
+    long long n1 = 0;
+    int f1 = 0;
+    double p = full_pdf<MODE, Stack>(x[i], Q, K, n1, f1);
+    if (f1 & kFlagExact) p = __builtin_nan("");  // near-tie: settled exactly below
+    flags |= f1 & kFlagErrors;
+    p = settle(p, x[i], Q, K, false, n1, flags);
+    ne += n1;
     lp[i] = node_logp(p, Q, K);
   }
-  if (ovf) atomicOr(status, ovf);
+  if (flags & kFlagErrors) atomicOr(status, flags & kFlagErrors);
   if (COUNT) {
     ne = wave_sum_ll(ne);
     if (threadIdx.x == 0) atomicAdd(evals, (unsigned long long)ne);
@@ -549,15 +636,13 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(const do
 
 // wiener_like_multi (wfpt.pyx:244-274): per-trial parameters, ±999 = missing.
 template <int STK>
-__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(const double* x, int64_t n,
-                                                       const double* const* arr,
-                                                       const double* scal, Knobs K,
-                                                       double p_outlier, double* out,
-                                                       int* zeros, int* status) {
+__global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(
+    const double* x, int64_t n, const double* const* arr, const double* scal, Knobs K,
+    double p_outlier, double* out, int* zeros, int* status) {
   using Stack = typename StackOf<STK>::type;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double lp = 0.0;
-  int zero = 0, ovf = 0;
+  int zero = 0, flags = 0;
   long long ne = 0;
   if (i < n) {
     double q[7];
@@ -575,8 +660,9 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(const do
     const double xi = x[i];
     double p;
     if (fabs(xi) != 999.) {
-      p = full_pdf<kRuntime, Stack, false>(xi, Q, K, ne, ovf);
-      if (ovf) atomicOr(status, ovf);
+      p = full_pdf<kRuntime, Stack>(xi, Q, K, ne, flags);
+      p = settle(p, xi, Q, K, !trial_setup(xi, Q).valid, ne, flags);
+      if (flags & kFlagErrors) atomicOr(status, flags & kFlagErrors);
       p = p * (1 - p_outlier) + (K.w_outlier * p_outlier);
     } else if (xi == 999.) {
       p = prob_ub(Q.v, Q.a, Q.z);
@@ -596,88 +682,6 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(const do
 // ---------------------------------------------------------------------------
 // launchers
 
-template <int MODE, int STK, bool COUNT, int OUT>
-static void launch_generic(const TrialArgs& A, int64_t nb, hipStream_t s) {
-  hipLaunchKernelGGL((trial_kernel<MODE, STK, COUNT, OUT>), dim3(nb), dim3(kBlock), 0, s, A);
-}
-
-// fast pass + (for adaptive modes) the slow pass on the deferred trials
-template <int MODE, int STK, bool COUNT, int OUT>
-static void launch_slow(const TrialArgs& A, int64_t nb, const unsigned char* wl, const int* wl_n,
-                        hipStream_t s) {
-  hipLaunchKernelGGL((slow_kernel<MODE, STK, COUNT, OUT>), dim3(slow_grid(nb)), dim3(64), 0, s, A,
-                     wl, wl_n, nb, nb);
-}
-
-template <int MODE, bool COUNT, int OUT>
-static void launch_two_pass(int stk, const TrialArgs& A, int64_t n, unsigned char* wl,
-                            int* wl_n, hipStream_t s, hipEvent_t fast_done) {
-  // both fast kernels leave one partial / worklist per 64 trials
-  constexpr int TPB = 64;
-  const int64_t nb = (n + TPB - 1) / TPB;
-  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(n)), dim3(kFastBlock), 0,
-                     s, A, wl, wl_n);
-  if (fast_done) (void)hipEventRecord(fast_done, s);
-  if (MODE == kDirect) return;
-  const int64_t g = slow_grid(nb);
-  if (stk == 0)
-    hipLaunchKernelGGL((slow_kernel<MODE, 0, COUNT, OUT>), dim3(g), dim3(TPB), 0, s, A, wl, wl_n,
-                       nb, nb);
-  else if (stk == 1)
-    hipLaunchKernelGGL((slow_kernel<MODE, 1, COUNT, OUT>), dim3(g), dim3(TPB), 0, s, A, wl, wl_n,
-                       nb, nb);
-  else
-    hipLaunchKernelGGL((slow_kernel<MODE, 2, COUNT, OUT>), dim3(g), dim3(TPB), 0, s, A, wl, wl_n,
-                       nb, nb);
-}
-
-template <bool COUNT, int OUT>
-static void launch_out(int mode, int stk, const TrialArgs& A, int64_t nb, unsigned char* wl,
-                       int* wl_n, hipStream_t s, hipEvent_t ev) {
-  switch (mode) {
-    case kDirect: launch_two_pass<kDirect, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
-    case kAdaptT: launch_two_pass<kAdaptT, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
-    case kAdaptZ: launch_two_pass<kAdaptZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
-    case kAdaptTZ: launch_two_pass<kAdaptTZ, COUNT, OUT>(stk, A, A.n, wl, wl_n, s, ev); break;
-    case kFixedT: launch_generic<kFixedT, 0, COUNT, OUT>(A, nb, s); break;
-    case kFixedZ: launch_generic<kFixedZ, 0, COUNT, OUT>(A, nb, s); break;
-    default: launch_generic<kFixedTZ, 0, COUNT, OUT>(A, nb, s); break;
-  }
-  if (ev && mode > kAdaptTZ) (void)hipEventRecord(ev, s);  // the single trial kernel
-}
-
-template <bool COUNT>
-static void launch_count(int out_kind, int mode, int stk, const TrialArgs& A, int64_t nb,
-                         unsigned char* wl, int* wl_n, hipStream_t s, hipEvent_t ev) {
-  if (out_kind == OUT_SUM) launch_out<COUNT, OUT_SUM>(mode, stk, A, nb, wl, wl_n, s, ev);
-  else if (out_kind == OUT_ARRAY) launch_out<COUNT, OUT_ARRAY>(mode, stk, A, nb, wl, wl_n, s, ev);
-  else launch_out<COUNT, OUT_LOGP>(mode, stk, A, nb, wl, wl_n, s, ev);
-}
-
-// Where launch_trials(OUT_SUM) leaves the partials finalize must sum: the
-// slow pass's G partials (which already fold the fast ones) for adaptive
-// modes, else every fast / trial-kernel partial.
-void final_partials(int64_t n, const Params& P, const Knobs& K, int64_t* off, int64_t* cnt) {
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  const int64_t nw = (n + 63) / 64;
-  if (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) {
-    *off = nw;
-    *cnt = slow_grid(nw);
-  } else {
-    *off = 0;
-    *cnt = (mode == kDirect) ? nw : blocks_for(n);
-  }
-}
-
-// size of the partial buffers launch_trials(OUT_SUM) writes
-int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  const int64_t nw = (n + 63) / 64;  // fast (and slow) partials are per 64 trials
-  if (mode == kAdaptT || mode == kAdaptZ || mode == kAdaptTZ) return nw + slow_grid(nw);
-  if (mode == kDirect) return nw;
-  return blocks_for(n);  // fixed Simpson: trial_kernel, one partial per 256-trial block
-}
-
 int stack_kind(const Knobs& K) {
   const int d = (K.n_st > K.n_sz) ? K.n_st : K.n_sz;
   return d <= 2 ? 0 : (d <= 4 ? 1 : 2);
@@ -685,9 +689,9 @@ int stack_kind(const Knobs& K) {
 
 int64_t blocks_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
 
-void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, const Knobs& K,
-                   double* out, int* zeros, unsigned long long* evals, int* status, int logp,
-                   unsigned char* wl, int* wl_n, hipStream_t s, hipEvent_t fast_done) {
+static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const Knobs& K,
+                            double* out, int* zeros, unsigned long long* evals, int* status,
+                            int logp) {
   TrialArgs A;
   A.x = x;
   A.n = n;
@@ -699,70 +703,103 @@ void launch_trials(int out_kind, const double* x, int64_t n, const Params& P, co
   A.evals = evals;
   A.status = status;
   A.logp = logp;
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  const int64_t nb = blocks_for(n);
-  if (nb == 0) return;
-  if (evals) launch_count<true>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s, fast_done);
-  else launch_count<false>(out_kind, mode, stack_kind(K), A, nb, wl, wl_n, s, fast_done);
-}
-
-static TrialArgs sum_args(const double* x, int64_t n, const Params& P, const Knobs& K,
-                          double* part, int* zeros, int* status) {
-  TrialArgs A;
-  A.x = x;
-  A.n = n;
-  A.P = P;
-  A.K = K;
-  A.wp_outlier = K.w_outlier * P.p_outlier;
-  A.out = part;
-  A.zeros = zeros;
-  A.evals = nullptr;
-  A.status = status;
-  A.logp = 0;
   return A;
 }
 
-bool launch_fast_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s,
-                      hipEvent_t fast_done) {
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  if (n <= 0 || mode < kAdaptT || mode > kAdaptTZ) return false;
-  const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
-  const dim3 g(fast_blocks(n)), b(kFastBlock);
-  switch (mode) {
-    case kAdaptT: hipLaunchKernelGGL((fast_kernel<kAdaptT, false, OUT_SUM>), g, b, 0, s, A, wl, wl_n); break;
-    case kAdaptZ: hipLaunchKernelGGL((fast_kernel<kAdaptZ, false, OUT_SUM>), g, b, 0, s, A, wl, wl_n); break;
-    default: hipLaunchKernelGGL((fast_kernel<kAdaptTZ, false, OUT_SUM>), g, b, 0, s, A, wl, wl_n); break;
-  }
+template <int MODE, bool COUNT, int OUT>
+static void run_fast(const TrialArgs& A, const Work& W, hipStream_t s, hipEvent_t fast_done) {
+  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock), 0,
+                     s, A, W);
   if (fast_done) (void)hipEventRecord(fast_done, s);
-  return true;
 }
 
-void launch_slow_pass(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                      int* zeros, int* status, unsigned char* wl, int* wl_n, hipStream_t s) {
-  const TrialArgs A = sum_args(x, n, P, K, part, zeros, status);
-  const int64_t nb = (n + 63) / 64;
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  const int stk = stack_kind(K);
-#define SLOW(M_)                                                        \
-  do {                                                                  \
-    if (stk == 0) launch_slow<M_, 0, false, OUT_SUM>(A, nb, wl, wl_n, s); \
-    else if (stk == 1) launch_slow<M_, 1, false, OUT_SUM>(A, nb, wl, wl_n, s); \
-    else launch_slow<M_, 2, false, OUT_SUM>(A, nb, wl, wl_n, s);        \
+template <int MODE, bool COUNT, int OUT>
+static void run_deferred(const TrialArgs& A, const Work& W, int depth, hipStream_t s) {
+  const int64_t nw = (A.n + 63) / 64;
+  if (MODE != kDirect && depth > 0) {
+    hipLaunchKernelGGL(gather_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, W.wl_n, nw, W);
+    const int lv = depth < kBfDepth ? depth : kBfDepth;
+    const int64_t gl = std::min<int64_t>(WFPT_LEVEL_GRID, (2 * nw * 64 + 255) / 256);
+    if (lv >= 1)
+      hipLaunchKernelGGL((level_kernel<MODE, 1, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
+    if (lv >= 2)
+      hipLaunchKernelGGL((level_kernel<MODE, (kBfDepth >= 2 ? 2 : 1), COUNT>), dim3(gl), dim3(256),
+                         0, s, A, W, depth);
+    if (lv >= 3)
+      hipLaunchKernelGGL((level_kernel<MODE, (kBfDepth >= 3 ? 3 : 1), COUNT>), dim3(gl), dim3(256),
+                         0, s, A, W, depth);
+  }
+  const int64_t gf = std::min<int64_t>(WFPT_FOLD_GRID, nw);
+  hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(64), 0, s, A, W, nw, depth);
+}
+
+template <bool COUNT, int OUT>
+static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, int depth,
+                        hipStream_t s, hipEvent_t fast_done) {
+#define FAST_AND_DEFERRED(M_)                                               \
+  do {                                                                      \
+    if (part & kPassFast) run_fast<M_, COUNT, OUT>(A, W, s, fast_done);     \
+    if (part & kPassDeferred) run_deferred<M_, COUNT, OUT>(A, W, depth, s); \
   } while (0)
   switch (mode) {
-    case kAdaptT: SLOW(kAdaptT); break;
-    case kAdaptZ: SLOW(kAdaptZ); break;
-    case kAdaptTZ: SLOW(kAdaptTZ); break;
-    default: break;  // kDirect never defers
+    case kDirect: FAST_AND_DEFERRED(kDirect); break;
+    case kAdaptT: FAST_AND_DEFERRED(kAdaptT); break;
+    case kAdaptZ: FAST_AND_DEFERRED(kAdaptZ); break;
+    case kAdaptTZ: FAST_AND_DEFERRED(kAdaptTZ); break;
+    case kFixedT:
+      hipLaunchKernelGGL((trial_kernel<kFixedT, COUNT, OUT>), dim3(blocks_for(A.n)), dim3(kBlock),
+                         0, s, A);
+      break;
+    case kFixedZ:
+      hipLaunchKernelGGL((trial_kernel<kFixedZ, COUNT, OUT>), dim3(blocks_for(A.n)), dim3(kBlock),
+                         0, s, A);
+      break;
+    default:
+      hipLaunchKernelGGL((trial_kernel<kFixedTZ, COUNT, OUT>), dim3(blocks_for(A.n)),
+                         dim3(kBlock), 0, s, A);
+      break;
   }
-#undef SLOW
+#undef FAST_AND_DEFERRED
+  if (fast_done && mode > kAdaptTZ) (void)hipEventRecord(fast_done, s);
 }
 
-void launch_finalize(const double* part, const int* zeros, int64_t nb, int* status, double* out,
-                     unsigned long long seq, hipStream_t s, int keep) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, status, out,
-                     seq, keep);
+static int tree_depth(const Params& P, const Knobs& K) {
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  return mode == kAdaptZ ? K.n_sz : K.n_st;
+}
+
+bool has_deferred_pass(const Params& P, const Knobs& K) {
+  return select_mode(P.sz, P.st, K.use_adaptive) <= kAdaptTZ;
+}
+
+int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
+  return has_deferred_pass(P, K) ? (n + 63) / 64 : blocks_for(n);
+}
+
+void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
+                   const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
+                   int logp, const Work& W, hipStream_t s, hipEvent_t fast_done) {
+  if (n <= 0) return;
+  const TrialArgs A = trial_args(x, n, P, K, out, zeros, evals, status, logp);
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  const int depth = tree_depth(P, K);
+  if (evals) {
+    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, depth, s, fast_done);
+    else if (out_kind == OUT_ARRAY)
+      launch_mode<true, OUT_ARRAY>(mode, part, A, W, depth, s, fast_done);
+    else launch_mode<true, OUT_LOGP>(mode, part, A, W, depth, s, fast_done);
+  } else {
+    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, depth, s, fast_done);
+    else if (out_kind == OUT_ARRAY)
+      launch_mode<false, OUT_ARRAY>(mode, part, A, W, depth, s, fast_done);
+    else launch_mode<false, OUT_LOGP>(mode, part, A, W, depth, s, fast_done);
+  }
+}
+
+void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
+                     int* status, double* out, unsigned long long seq, hipStream_t s) {
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, wl_n, nw, status,
+                     out, seq);
 }
 
 template <int MODE, bool COUNT>
@@ -771,8 +808,7 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                                   Params* d_par, int* n_defer, unsigned long long* evals,
                                   int* status, hipStream_t s) {
   hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
-                     node, n, P, K, lp, d_idx, d_par, n_defer, evals);
-  if (MODE == kDirect) return;
+                     node, n, P, K, lp, d_idx, d_par, n_defer, evals, status);
   const int64_t nl = (n + 63) / 64;
   const int64_t g = nl < 2048 ? nl : 2048;
   const int stk = stack_kind(K);

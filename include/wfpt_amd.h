@@ -124,10 +124,21 @@ int wfpt_dmat_cdf_array(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_pa
 int wfpt_comm_unique_id(unsigned char id[128]);
 int wfpt_comm_init(wfpt_ctx *ctx, int nranks, int rank, const unsigned char id[128]);
 /* wiener_like over this rank's resident shard, combined across ranks with one
- * ncclAllReduce of {sum log p, #zero trials} (2 doubles); every rank receives
- * the global total. */
+ * ncclAllReduce of 3 doubles {sum log p, #zero-density trials, encoded error
+ * counts}; every rank receives the global total (-inf if any rank holds a
+ * zero-density trial) or every rank fails with the same WFPT_ERR_UNSUPPORTED
+ * if any rank exceeded the depth / evaluation limits. */
 int wfpt_wiener_like_allreduce(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
                                const wfpt_knobs *k, double *out_logp);
+
+/* Decodes a likelihood result triple {sum of log p over trials with nonzero
+ * density, #zero-density trials, encoded error counts} — the 3 doubles that
+ * wfpt_wiener_like_allreduce sums over ranks — into the reference's value:
+ * -inf if any trial had zero density (wfpt.pyx:71-72), else the sum; a nonzero
+ * error count returns WFPT_ERR_UNSUPPORTED naming each error kind. Error
+ * encoding: (#ranks past WFPT_MAX_DEPTH) + 1048576 * (#ranks past
+ * WFPT_EVAL_BUDGET), so kinds stay apart under the sum. */
+int wfpt_decode_result(const double r[3], double *out_logp);
 
 /* ---- measurement -------------------------------------------------------- */
 /* flags & WFPT_PROF_EVENTS: bracket the main likelihood kernel of each call

@@ -1,10 +1,11 @@
-"""world_size-2 gloo test of the sharded likelihood's host logic (CPU).
+"""world_size-2 gloo tests of the sharded likelihood's combine (CPU).
 
 Each rank takes its contiguous shard (hddm_amd.dist.shard_range, the C ABI's
-wfpt_shard_range), computes its {sum log p, #zero trials} partial with the
-oracle (standing in for the per-GPU kernel, which needs a device), and the two
-partials are all-reduced over gloo exactly as libwfpt_amd all-reduces them
-over RCCL. The combined value must equal the unsharded reference likelihood.
+wfpt_shard_range), computes its {sum log p, #zero trials, encoded errors}
+triple with the oracle (standing in for the per-GPU kernels, which need a
+device), the triples are summed over gloo exactly as libwfpt_amd sums them
+over RCCL, and the library's own decode (wfpt_decode_result) turns the sum into
+the value or the error every rank reports.
 """
 import math
 import os
@@ -25,12 +26,13 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, x, args, kn, out_q):
+def _worker(rank, world, port, x, args, kn, inject, out_q):
     import sys
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
     import oracle
+    from hddm_amd import _lib
     from hddm_amd import dist as hdist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -38,40 +40,77 @@ def _worker(rank, world, port, x, args, kn, out_q):
     lo, hi = hdist.shard_range(x.size, world, rank)
     lp = oracle.pdf_array(x[lo:hi], *args, kn[0], 1, *kn[1:])
     zeros = int(np.isneginf(lp).sum())
-    s = math.fsum(lp[np.isfinite(lp)]) if zeros == 0 else 0.0
-    t = torch.tensor([s, float(zeros)], dtype=torch.float64)
-    dist.all_reduce(t)  # the {sum, zeros} part of RCCL's 3-double sum in wfpt_wiener_like_allreduce
-    total = -math.inf if t[1].item() > 0 else t[0].item()
-    out_q.put((rank, total, hi - lo))
+    s = math.fsum(lp[np.isfinite(lp)])
+    # this rank's {sum, zeros, encoded errors} triple, as finalize_kernel writes
+    # it; the sum over ranks is what wfpt_wiener_like_allreduce's ncclAllReduce does
+    err = inject.get(rank, 0.0)
+    t = torch.tensor([s, float(zeros), err], dtype=torch.float64)
+    dist.all_reduce(t)
+    try:
+        res = ("ok", _lib.decode_result(t.tolist()))  # the library's decode
+    except NotImplementedError as e:
+        res = ("error", str(e))
+    out_q.put((rank, res, hi - lo))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("inject_zero", [False, True])
-def test_two_rank_allreduce_matches_unsharded(oracle_lib, inject_zero):
-    rng = np.random.default_rng(1)
-    x = rng.choice([-1.0, 1.0], 3001) * (0.35 + rng.gamma(2.0, 0.4, 3001))
-    if inject_zero:
-        x[2900] = 0.1  # below t - st/2: zero density on rank 1 only
-    args = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
-    kn = (1e-4, 2, 2, 1, 1e-3, 0.0, 0.1)
+def _run(x, args, kn, inject):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, x, args, kn, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, x, args, kn, inject, q))
+             for r in range(2)]
     for p in procs:
         p.start()
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = oracle_lib.wiener_like(x, *args, *kn)
     assert sum(r[2] for r in res) == x.size
-    for _, total, _ in res:
+    return [r[1] for r in res]
+
+
+@pytest.mark.parametrize("inject_zero", [False, True])
+def test_two_rank_allreduce_matches_unsharded(oracle_lib, inject_zero):
+    """World-2 gloo: shard, per-rank triple, sum over ranks, the library's
+    decode. Equals the unsharded reference; a zero-density trial on one rank
+    gives -inf on every rank (wfpt.pyx:71-72)."""
+    rng = np.random.default_rng(1)
+    x = rng.choice([-1.0, 1.0], 3001) * (0.35 + rng.gamma(2.0, 0.4, 3001))
+    if inject_zero:
+        x[2900] = 0.1  # below t - st/2: zero density on rank 1 only
+    args = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.0, 0.1)
+    res = _run(x, args, kn, {})
+    ref = oracle_lib.wiener_like(x, *args, *kn)
+    for kind, total in res:
+        assert kind == "ok"
         if inject_zero:
             assert total == -math.inf and ref == -math.inf
         else:
             assert abs(total - ref) < 1e-9 * abs(ref)
+
+
+@pytest.mark.parametrize("inject,want", [
+    ({0: 1.0}, ["WFPT_MAX_DEPTH"]),                          # depth error on rank 0 only
+    ({0: 1.0, 1: 1.0}, ["WFPT_MAX_DEPTH"]),                  # on both: still depth, not budget
+    ({1: 1048576.0}, ["WFPT_EVAL_BUDGET"]),                  # budget error on rank 1
+    ({0: 1.0, 1: 1048576.0}, ["WFPT_MAX_DEPTH", "WFPT_EVAL_BUDGET"]),
+])
+def test_two_rank_error_propagation(inject, want):
+    """A depth / budget failure on any rank fails every rank, and the two kinds
+    stay distinguishable after the sum over ranks (summed bit flags
+    made two depth errors read as a budget error)."""
+    rng = np.random.default_rng(2)
+    x = rng.choice([-1.0, 1.0], 500) * (0.35 + rng.gamma(2.0, 0.4, 500))
+    res = _run(x, (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0), (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1), inject)
+    for kind, msg in res:
+        assert kind == "error"
+        for w in want:
+            assert w in msg
+        for w in {"WFPT_MAX_DEPTH", "WFPT_EVAL_BUDGET"} - set(want):
+            assert w not in msg
 
 
 @pytest.mark.gpu

@@ -19,57 +19,41 @@ TOTAL_RTOL = 1e-11  # totals, relative to sum |log p|
 
 
 def assert_density_parity(gpu, ref, what=""):
+    """Per-trial densities: |log p_gpu - log p_ref| < 1e-6 for every positive
+    reference density, subnormal ones included (no relaxation); zeros, NaNs
+    and signs match exactly; negative densities (the large-time series can
+    dip below zero) agree in log|p| to the same bar."""
     gpu = np.asarray(gpu, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     assert gpu.shape == ref.shape
     nan_r, nan_g = np.isnan(ref), np.isnan(gpu)
-    assert np.array_equal(nan_r, nan_g), f"{what}: NaN pattern differs"
+    assert np.array_equal(nan_r, nan_g), f"{what}: NaN pattern differs at {np.flatnonzero(nan_r != nan_g)[:10]}"
     zr, zg = ref == 0, gpu == 0
     bad = np.flatnonzero(zr != zg)
     assert bad.size == 0, f"{what}: zero pattern differs at {bad[:10]} ref={ref[bad[:5]]} " \
                           f"gpu={gpu[bad[:5]]}"
-    pos = (ref > 0) & ~nan_r
-    assert np.all(gpu[pos] > 0), f"{what}: sign differs"
-    normal = pos & (ref > 1e-290)
-    d = np.abs(np.log(gpu[normal]) - np.log(ref[normal]))
-    assert d.size == 0 or d.max() < LOGP_TOL, f"{what}: max |dlogp| = {d.max():.3e}"
-    tiny = pos & ~normal
-    assert np.all(np.abs(gpu[tiny] - ref[tiny]) < 1e-300)
-    sub = pos & (ref < np.finfo(np.float64).tiny)
-    assert np.all(np.abs(gpu[sub] - ref[sub]) <= subnormal_tol(ref[sub])), f"{what}: subnormal"
-
-    neg = (ref < 0) & ~nan_r  # the large-t series can go (slightly) negative
-    if neg.any():
-        np.testing.assert_allclose(gpu[neg], ref[neg], rtol=1e-9, atol=1e-300)
-
-
-LOG_DBL_MIN = np.log(np.finfo(np.float64).tiny)  # -708.4
-SUBNORMAL_ATOL = 8 * 4.9406564584124654e-324     # 8 subnormal ulps
-
-
-def subnormal_tol(p):
-    """|dp| allowed for a reference density p below DBL_MIN: the north_star's
-    |d log p| < 1e-6 (i.e. 1e-6 relative) or, deep in the subnormal range where
-    the reference's own value is quantised coarser than that, 8 subnormal ulps."""
-    return np.maximum(SUBNORMAL_ATOL, LOGP_TOL * np.abs(p))
+    nz = ~nan_r & ~zr
+    assert np.array_equal(np.sign(gpu[nz]), np.sign(ref[nz])), f"{what}: sign differs"
+    with np.errstate(divide="ignore"):
+        d = np.abs(np.log(np.abs(gpu[nz])) - np.log(np.abs(ref[nz])))
+    if d.size:
+        k = int(np.argmax(d))
+        assert d[k] < LOGP_TOL, f"{what}: max |dlogp| = {d[k]:.3e} (ref {ref[nz][k]:.6e}, " \
+                                f"gpu {gpu[nz][k]:.6e})"
 
 
 def assert_logp_parity(gpu, ref, what=""):
-    """|dlogp| < 1e-6 per trial. A density below DBL_MIN is quantised to the
-    subnormal grid (relative spacing up to 1e-5 near 1e-319) in the reference
-    itself, so there parity is |dp| <= max(8 subnormal ulps, 1e-6 p)."""
+    """|dlogp| < 1e-6 per trial, everywhere (log densities of subnormal
+    densities included); NaN and -inf patterns exact."""
     gpu = np.asarray(gpu, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
     assert np.array_equal(np.isnan(gpu), np.isnan(ref)), f"{what}: NaN pattern"
     assert np.array_equal(np.isneginf(gpu), np.isneginf(ref)), f"{what}: -inf pattern"
     fin = np.isfinite(ref)
-    sub = fin & (ref < LOG_DBL_MIN)
-    nrm = fin & ~sub
-    d = np.abs(gpu[nrm] - ref[nrm])
-    assert d.size == 0 or d.max() < LOGP_TOL, f"{what}: max |dlogp| = {d.max():.3e}"
-    ds = np.abs(np.exp(gpu[sub]) - np.exp(ref[sub]))
-    ok = ds <= subnormal_tol(np.exp(ref[sub]))
-    assert ok.all(), f"{what}: subnormal |dp| {ds.max()}"
+    d = np.abs(gpu[fin] - ref[fin])
+    if d.size:
+        k = int(np.argmax(d))
+        assert d[k] < LOGP_TOL, f"{what}: max |dlogp| = {d[k]:.3e} (ref {ref[fin][k]:.6e})"
 
 
 def assert_total(gpu, ref_terms, what=""):
