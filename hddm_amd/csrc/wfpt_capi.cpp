@@ -109,10 +109,11 @@ struct wfpt_ctx {
   DevBuf<unsigned char> wl;  // lane of the deferred trial in each slot
   DevBuf<int> wl_n;          // per chunk: #tree | #exact << 8
   DevBuf<int> rflag;         // per slot: kFlag*
+  DevBuf<unsigned> pend;     // per slot: tree points awaiting z refinement
   DevBuf<double> tf;         // per slot: tree sample values (SoA)
   DevBuf<int> rcnt;          // per slot: evaluation counts (PROF_EVALS only)
   DevBuf<uint32_t> tasks;    // tree-level task lists
-  int* ntask = nullptr;      // device: 8 task counters (0 at rest)
+  int* ntask = nullptr;      // device: 16 list lengths (0 at rest)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
@@ -218,12 +219,14 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   HIP_TRY(c->wl.reserve(ns));
   HIP_TRY(c->wl_n.reserve(nw));
   HIP_TRY(c->rflag.reserve(ns));
+  HIP_TRY(c->pend.reserve(ns));
   HIP_TRY(c->tf.reserve(ns * wfpt::kTreePoints));
   HIP_TRY(c->tasks.reserve(wfpt::task_capacity(ns)));
   if (c->count) HIP_TRY(c->rcnt.reserve(ns));
   W->wl = c->wl.p;
   W->wl_n = c->wl_n.p;
   W->rflag = c->rflag.p;
+  W->pend = c->pend.p;
   W->F = c->tf.p;
   W->rcnt = c->count ? c->rcnt.p : nullptr;
   W->tasks = c->tasks.p;
@@ -417,8 +420,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
-  if (e == hipSuccess) e = hipMalloc((void**)&c->ntask, 8 * sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->ntask, 0, 8 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->ntask, 16 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->ntask, 0, 16 * sizeof(int));
   if (e == hipSuccess) std::memset(c->mres, 0, 5 * sizeof(double));
   if (e != hipSuccess) {
     wfpt_close(c);
@@ -444,6 +447,7 @@ void wfpt_close(wfpt_ctx* c) {
   c->wl.release();
   c->wl_n.release();
   c->rflag.release();
+  c->pend.release();
   c->tf.release();
   c->rcnt.release();
   c->tasks.release();

@@ -355,8 +355,41 @@ __device__ inline bool simpson_refine(double S, double S2, double err, int botto
 // ---------------------------------------------------------------------------
 // Adaptive Simpson (integrate.pxi:72-141, 143-206) as an iterative walk.
 struct Frame {
-  double lb, ub, S, fb, fe, fm, err, left;
+  double lb, ub, S, fb, fe, fm, err, left, hs;
 };
+
+// Tie resolution inside a per-lane walk. A stop test decided within kTieBand
+// is re-decided from the interval's 5 points evaluated on the exact path
+// (literal expressions, glibc-equal libm): the reference's own S and S2, so
+// only that decision pays exact evaluations (deep trees run ~1e5 tests per
+// trial, where whole-trial exact recomputation would dominate). NoResolve
+// instead abandons the trial (kFlagExact: the caller recomputes it exactly).
+struct NoResolve {
+  static constexpr bool kResolves = false;
+  __device__ bool operator()(double, double, double, bool, double, int) const { return false; }
+};
+template <class GX>
+struct XResolve {
+  static constexpr bool kResolves = true;
+  GX gx;  // exact f(u), the reference's integrand value (divided by its width)
+  // [lb, ub]: the interval; its S came from (hs / 6) (root prologue) or
+  // (hs / 12) (a parent's Sleft / Sright, hs = the parent's width), each over
+  // (f(lb) + 4 f(c)) + f(ub) (integrate.pxi:133-134, 105-107).
+  __device__ bool operator()(double lb, double ub, double hs, bool root, double err,
+                             int bottom) const {
+    const double c = (ub + lb) / 2.;
+    const double d = (lb + c) / 2., e = (c + ub) / 2.;
+    const double fb = gx(lb), fd = gx(d), fm = gx(c), fe = gx(e), fu = gx(ub);
+    const double S = root ? (hs / 6) * ((fb + (4 * fm)) + fu) : (hs / 12) * ((fb + (4 * fm)) + fu);
+    const double h = ub - lb;
+    const double S2 = ((h / 12) * ((fb + (4 * fd)) + fm)) + ((h / 12) * ((fm + (4 * fe)) + fu));
+    return !(bottom <= 0 || fabs(S2 - S) <= 15 * err);
+  }
+};
+template <class GX>
+__device__ inline XResolve<GX> make_xresolve(GX gx) {
+  return XResolve<GX>{gx};
+}
 
 // Depth <= N frames held in registers: every access is a compile-time index
 // after unrolling, so the array is scalarised (no scratch).
@@ -405,20 +438,20 @@ constexpr long long kEvalBudget = 1ll << 24;
 
 // Integrates g over [lb0, ub0] exactly like adaptiveSimpsons_1D/_2D followed by
 // adaptiveSimpsonsAux(_2D): g(c) must already include the division by ZT (or
-// st). With init == false the walk starts at the aux node (lb0, ub0, S0, fb0,
-// fe0, fm0) instead (a refinement resumed from known values). Every lane walks
-// its own tree; each loop trip evaluates g at the 3 prologue nodes or the 2
-// new nodes of one interval from ONE call site. Depth past the stack, the
-// evaluation budget or a near-tie stop test abandon the trial (flags set,
-// NaN returned): no input keeps a wave busy without bound.
-template <class Stack, class G>
+// st). Every lane walks its own tree; each loop trip evaluates g at the 3
+// prologue nodes or the 2 new nodes of one interval from ONE call site. A
+// near-tie stop test is re-decided by `resolve` (XResolve) or abandons the
+// trial (NoResolve); depth past the stack or the evaluation budget abandon it
+// too (flags set, NaN returned): no input keeps a wave busy without bound.
+template <class Stack, class G, class R = NoResolve>
 __device__ inline double adaptive_walk(G&& g, double lb0, double ub0, double err0, int depth,
-                                       int& flags, const long long& ne, bool init = true,
-                                       double S0 = 0.0, double fb0 = 0.0, double fe0 = 0.0,
-                                       double fm0 = 0.0) {
+                                       int& flags, const long long& ne, const R& resolve = R()) {
   Stack stk;
   double lb = lb0, ub = ub0, err = err0;
-  double S = S0, fb = fb0, fe = fe0, fm = fm0;
+  double S = 0.0, fb = 0.0, fe = 0.0, fm = 0.0;
+  double hs = 0.0;    // width the current S was computed with
+  bool sroot = true;  // S from the prologue (hs / 6) rather than a parent (hs / 12)
+  bool init = true;
   int bottom = depth, sp = 0;
   unsigned right_mask = 0u;  // bit i: frame i has finished its left child
   double result = 0.0;
@@ -447,6 +480,8 @@ __device__ inline double adaptive_walk(G&& g, double lb0, double ub0, double err
       fe = y1;
       fm = y2;
       S = (h / 6) * ((fb + (4 * fm)) + fe);
+      hs = h;
+      sroot = true;
       init = false;
       continue;
     }
@@ -455,10 +490,14 @@ __device__ inline double adaptive_walk(G&& g, double lb0, double ub0, double err
     const double Sl = (h / 12) * ((fb + (4 * fd)) + fm);
     const double Sr = (h / 12) * ((fm + (4 * fee)) + fe);
     const double S2 = Sl + Sr;
-    const bool refine = simpson_refine(S, S2, err, bottom, flags);
+    bool refine = simpson_refine(S, S2, err, bottom, flags);
     if (flags & kFlagExact) {
-      result = __builtin_nan("");
-      break;
+      if (!R::kResolves) {
+        result = __builtin_nan("");
+        break;
+      }
+      flags &= ~kFlagExact;
+      refine = resolve(lb, ub, hs, sroot, err, bottom);
     }
     if (refine && sp >= Stack::kCap) {
       flags |= kFlagDepth;
@@ -475,11 +514,14 @@ __device__ inline double adaptive_walk(G&& g, double lb0, double ub0, double err
       fr.fm = fee;
       fr.err = err / 2;
       fr.left = 0.0;
+      fr.hs = h;
       stk.set(sp, fr);
       ++sp;
       ub = c;
       err = err / 2;
       S = Sl;
+      hs = h;
+      sroot = false;
       fe = fm;
       fm = fd;
       bottom -= 1;
@@ -505,6 +547,8 @@ __device__ inline double adaptive_walk(G&& g, double lb0, double ub0, double err
         fe = fr.fe;
         fm = fr.fm;
         err = fr.err;
+        hs = fr.hs;
+        sroot = false;
         bottom = depth - sp;
         break;
       }
@@ -623,7 +667,9 @@ __device__ inline double full_pdf(double x0, const Params& P, const Knobs& K, lo
       ++ne;
       return tnode_pdf_sv(T, zc, v, sv, a) * iZT;
     };
-    return adaptive_walk<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, flags, ne);
+    const double ZT = ub_z - lb_z;
+    auto rz = make_xresolve([=](double zc) { return wfpt_x::pdf_sv(x - t, v, sv, a, zc, err) / ZT; });
+    return adaptive_walk<Stack>(g, lb_z, ub_z, K.simps_err, K.n_sz, flags, ne, rz);
   }
   if (mode == kAdaptT) {
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
@@ -632,12 +678,17 @@ __device__ inline double full_pdf(double x0, const Params& P, const Knobs& K, lo
       ++ne;
       return pdf_sv(x - tc, v, sv, a, z, err, flags) * iZT;
     };
-    return adaptive_walk<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, flags, ne);
+    const double ZT = ub_t - lb_t;
+    auto rt = make_xresolve([=](double tc) { return wfpt_x::pdf_sv(x - tc, v, sv, a, z, err) / ZT; });
+    return adaptive_walk<Stack>(g, lb_t, ub_t, K.simps_err, K.n_st, flags, ne, rt);
   }
   if (mode == kAdaptTZ) {
     const double lb_z = z - sz / 2., ub_z = z + sz / 2.;
     const double lb_t = t - st / 2., ub_t = t + st / 2.;
     const double iZT = 1.0 / (ub_z - lb_z), istw = 1.0 / (ub_t - lb_t);
+    const double ZT = ub_z - lb_z, stw = ub_t - lb_t;
+    const double se = K.simps_err;
+    const int nsz = K.n_sz;
     auto outer = [&](double tc) -> double {
       const TNode T = tnode_setup(x - tc, v, sv, a, err);
       if (T.amb) flags |= kFlagExact;
@@ -645,9 +696,16 @@ __device__ inline double full_pdf(double x0, const Params& P, const Knobs& K, lo
         ++ne;
         return tnode_pdf_sv(T, zc, v, sv, a) * iZT;
       };
-      return adaptive_walk<Stack>(inner, lb_z, ub_z, K.simps_err, K.n_sz, flags, ne) * istw;
+      auto rz = make_xresolve([=](double zc) { return wfpt_x::pdf_sv(x - tc, v, sv, a, zc, err) / ZT; });
+      return adaptive_walk<Stack>(inner, lb_z, ub_z, se, nsz, flags, ne, rz) * istw;
     };
-    return adaptive_walk<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, flags, ne);
+    // exact outer values: the reference's z integral at tc (its own walk)
+    auto rt = make_xresolve([=](double tc) {
+      wfpt_x::Ctx C;
+      auto inner_x = [&](double zc) { return wfpt_x::pdf_sv(x - tc, v, sv, a, zc, err) / ZT; };
+      return wfpt_x::adaptive(inner_x, lb_z, ub_z, se, nsz, C) / stw;
+    });
+    return adaptive_walk<Stack>(outer, lb_t, ub_t, K.simps_err, K.n_st, flags, ne, rt);
   }
   if (mode == kFixedT)
     return simpson_1d(x, v, sv, a, z, t, err, z, z, 0, t - st / 2., t + st / 2., K.n_st, ne,
@@ -900,18 +958,24 @@ constexpr int kBfDepth = WFPT_BF_DEPTH;
 constexpr int kTreeW = 4 << kBfDepth;
 constexpr int kTreePoints = kTreeW + 1;
 
-// Level-L task lists, levels 1..kBfDepth back to back: level l holds up to
-// 2^l tasks per slot.
-__host__ __device__ inline int64_t task_offset(int L, int64_t nslots) {
+// Task lists of the breadth-first levels, back to back: node lists N_L
+// (L = 1..kBfDepth: intervals to evaluate, up to 2^L per slot) then
+// repair lists RT_L (L = 0..kBfDepth: intervals whose z integrals need
+// refinement before their stop test, up to 2^L per slot). An entry is
+// slot << kBfDepth | m (m: the interval's index within its level).
+__host__ __device__ inline int64_t node_list(int L, int64_t nslots) {
   return ((int64_t(1) << L) - 2) * nslots;
 }
-__host__ __device__ inline int64_t task_capacity(int64_t nslots) {
-  return ((int64_t(1) << (kBfDepth + 1)) - 2) * nslots;
+__host__ __device__ inline int64_t repair_list(int L, int64_t nslots) {
+  return ((int64_t(1) << (kBfDepth + 1)) - 2 + (int64_t(1) << L) - 1) * nslots;
 }
+__host__ __device__ inline int64_t task_capacity(int64_t nslots) {
+  return ((int64_t(1) << (kBfDepth + 2)) - 3) * nslots;
+}
+// task counters (Work::ntask): N_L at [L], RT_L at [8 + L]
+constexpr int kRepairCounter = 8;
 
-// kFall: continue the whole trial on the per-lane walk (a z tree deeper than
-// kInnerCap inside a t tree).
-enum Outcome : int { kFinal = 0, kTree = 1, kExact = 2, kFall = 3 };
+enum Outcome : int { kFinal = 0, kTree = 1, kExact = 2 };
 
 // The reference's Simpson estimates of one interval from its 5 values.
 struct Simp {
@@ -944,23 +1008,17 @@ __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, 
   return s.S2 + (s.S2 - s.S) / 15;
 }
 
-// The complete z integral at one t node (root + refinement), inline and
-// register-light: a per-lane walk with a kInnerCap-frame register stack
-// (n_sz <= kInnerCap; deeper z trees go to the per-lane fallback with the
-// whole trial, kFlagFallback). Counts its root evaluations again.
-constexpr int kInnerCap = 3;
+// The complete z integral at one t node (root + refinement): a per-lane walk
+// (the repair kernels run it with a scratch stack, any n_sz <= WFPT_MAX_DEPTH).
+template <class Stack>
 __device__ inline double inner_full(const TNode& T, double lbz, double ubz, double iZz, double v,
                                     double sv, double a, const Knobs& K, int& flags,
                                     long long& ne) {
-  if (K.n_sz > kInnerCap) {
-    flags |= kFlagFallback;
-    return 0.0;
-  }
   auto g = [&](double zc) -> double {
     ++ne;
     return tnode_pdf_sv(T, zc, v, sv, a) * iZz;
   };
-  return adaptive_walk<RegStack<kInnerCap>>(g, lbz, ubz, K.simps_err, K.n_sz, flags, ne);
+  return adaptive_walk<Stack>(g, lbz, ubz, K.simps_err, K.n_sz, flags, ne);
 }
 
 // Root interval of the adaptive tree: over t for kAdaptT / kAdaptTZ, over z
@@ -980,15 +1038,17 @@ __device__ inline void tree_root(const Trial& tr, const Params& P, double& lb, d
 // prologue + root aux node of every adaptive Simpson it runs (1, 5, 5 or 25
 // pdf_sv evaluations, + refinements of the z integrals in kAdaptTZ).
 //   kFinal: p is the trial density (0 for invalid parameters);
-//   kTree:  the root stop test asks for refinement; f[] = the root interval's
-//           values at lb, d, c, e, ub (continued by the level kernels);
-//   kExact: the value hinges on last-bit rounding (recomputed exactly);
-//   kFall:  continue on the per-lane walk.
+//   kTree:  the root stop test asks for refinement, or (kAdaptTZ) some t
+//           node's z integral needs refinement first (bit k of `pend`: tree
+//           point k * kTreeW / 4; the root test then runs after the repair
+//           pass); f[] = the root interval's values at lb, d, c, e, ub;
+//   kExact: the value hinges on last-bit rounding (recomputed exactly).
 template <int MODE>
 __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, double& p,
-                                  double (&f)[5], long long& ne, int& flags) {
+                                  double (&f)[5], long long& ne, int& flags, unsigned& pend) {
   const Trial tr = trial_setup(x0, P);
   p = 0.0;
+  pend = 0u;
   if (!tr.valid) return kFinal;
   const double a = P.a, sv = P.sv, t = P.t, err = K.err;
   const double x = tr.x, v = tr.v, z = tr.z;
@@ -1016,7 +1076,6 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
     const double d = (lb + c) / 2., e = (c + ub) / 2.;
     const double lbz = z - tr.sz / 2., ubz = z + tr.sz / 2.;
     const double iZz = (MODE == kAdaptTZ) ? 1.0 / (ubz - lbz) : 0.0;
-    unsigned repair = 0u;  // t nodes whose z integral needs refinement
     {
       ZGrid G;
       if (MODE == kAdaptTZ) G = zgrid_setup(lbz, ubz, v, sv, a);
@@ -1064,7 +1123,7 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
           bool rep;
           y = inner_root(T, G, iZz, v, sv, a, K, flags, ne, rep) * iw;
           if (flags & kFlagExact) return kExact;
-          if (rep) repair |= 1u << j;
+          if (rep) pend |= 1u << (j * (kTreeW / 4));
         } else {
           ne += 1;
           y = tnode_pdf_sv(T, z, v, sv, a) * iw;
@@ -1076,24 +1135,8 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
         else f[4] = y;
       }
     }
-    // z integrals whose root test asked for refinement, after the loop (few
-    // live registers here): the complete walk at that t node
-    if (MODE == kAdaptTZ) {
-      while (repair) {
-        const int j = __builtin_ctz(repair);
-        repair &= repair - 1u;
-        const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
-        const TNode T = tnode_setup(x - tc, v, sv, a, err);
-        ne -= 5;  // inner_full evaluates the root again
-        const double y = inner_full(T, lbz, ubz, iZz, v, sv, a, K, flags, ne) * iw;
-        if (flags & kFlagExact) return kExact;
-        if (flags & (kFlagFallback | kFlagErrors)) return kFall;
-#pragma unroll
-        for (int k = 0; k < 5; ++k)
-          if (k == j) f[k] = y;
-      }
-    }
   }
+  if (pend) return kTree;  // root test after the z-integral repairs
   const Simp s = simp5(ub - lb, f[0], f[1], f[2], f[3], f[4]);
   const int bottom = (MODE == kAdaptZ) ? K.n_sz : K.n_st;
   const bool refine = simpson_refine(s.S, s.S2, K.simps_err, bottom, flags);
@@ -1144,11 +1187,13 @@ struct TreeFn {
     }
     return inner_root(T, G, iZz, tr.v, P.sv, P.a, K, flags, ne, repair) * iw;
   }
+  // kAdaptTZ: the complete z integral at t node u (repair kernels)
   __device__ inline double full(double u, const Params& P, const Knobs& K, int& flags,
                                 long long& ne) const {
     const TNode T = tnode_setup(tr.x - u, tr.v, P.sv, P.a, K.err);
-    ne -= 5;
-    return inner_full(T, lbz, ubz, iZz, tr.v, P.sv, P.a, K, flags, ne) * iw;
+    if (T.amb) flags |= kFlagExact;
+    return inner_full<MemStack<WFPT_MAX_DEPTH>>(T, lbz, ubz, iZz, tr.v, P.sv, P.a, K, flags, ne) *
+           iw;
   }
 };
 

@@ -19,13 +19,14 @@ struct Work {
   unsigned char* wl;  // [nslots] lane of the trial in slot
   int* wl_n;          // [chunks] #tree | #exact << 8 deferred trials of the chunk
   int* rflag;         // [nslots] kFlag* of the trial in slot
-  double* F;          // [tree_points() * nslots] tree sample values (SoA)
+  unsigned* pend;     // [nslots] tree points whose z integral awaits refinement
+  double* F;          // [kTreePoints * nslots] tree sample values (SoA)
   int* rcnt;          // [nslots] pdf_sv evaluations so far (evaluation counting only)
-  uint32_t* tasks;    // [task_capacity(nslots)] tree-level task lists
-  int* ntask;         // [8] task counts per level (0 at rest)
+  uint32_t* tasks;    // [task_capacity(nslots)] node and repair lists
+  int* ntask;         // [16] list lengths (0 at rest)
   int64_t nslots;
 };
-// task_offset / task_capacity / kTreePoints: wfpt_device.hpp
+// node_list / repair_list / task_capacity / kTreePoints: wfpt_device.hpp
 
 // Error flags encoded as counts in one double that survives an RCCL sum:
 // (#ranks with a depth error) + kBudgetUnit * (#ranks with a budget error).

@@ -57,7 +57,7 @@ struct FastWaves {
 #define WFPT_LEVEL_GRID 2048
 #endif
 #ifndef WFPT_FOLD_GRID
-#define WFPT_FOLD_GRID 2048
+#define WFPT_FOLD_GRID 16384
 #endif
 
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
@@ -139,20 +139,22 @@ void fast_kernel(TrialArgs A, Work W) {
   double p = 0.0, f[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   long long ne = 0;
   int flags = 0, oc = kFinal;
-  if (i < A.n) oc = fast_level0<MODE>(A.x[i], A.P, A.K, p, f, ne, flags);
+  unsigned pend = 0u;
+  if (i < A.n) oc = fast_level0<MODE>(A.x[i], A.P, A.K, p, f, ne, flags, pend);
   double lp = 0.0;
   int zero = 0;
   if (i < A.n && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
-  // tree records first, then exact / per-lane-walk records
-  const unsigned long long bt = __ballot(oc == kTree), be = __ballot(oc >= kExact);
+  // tree records first, then exact records
+  const unsigned long long bt = __ballot(oc == kTree), be = __ballot(oc == kExact);
   const int nt = __popcll(bt);
   if (oc != kFinal) {
     const int k = oc == kTree ? __popcll(bt & lanemask_lt(lane))
                               : nt + __popcll(be & lanemask_lt(lane));
     const int64_t slot = c * 64 + k;
     W.wl[slot] = (unsigned char)lane;
-    W.rflag[slot] = oc == kExact ? (int)kFlagExact : (oc == kFall ? (int)kFlagFallback : 0);
+    W.rflag[slot] = oc == kExact ? (int)kFlagExact : 0;
     if (oc == kTree) {
+      W.pend[slot] = pend;
 #pragma unroll
       for (int j = 0; j < 5; ++j) W.F[(int64_t)(j * (kTreeW / 4)) * W.nslots + slot] = f[j];
     }
@@ -173,55 +175,119 @@ void fast_kernel(TrialArgs A, Work W) {
   }
 }
 
-// Level-1 tasks (both halves of every tree record's root interval) from the
-// per-chunk tree counts: one wave per 64 chunks, one atomic per wave.
-__global__ __launch_bounds__(256) void gather_kernel(const int* wl_n, int64_t nw, Work W) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const int nt = c < nw ? (wl_n[c] & 255) : 0;
-  // wave inclusive prefix of 2 * nt
-  int v = 2 * nt;
+// Work lists of the tree records after the level-0 pass: a record whose root
+// test asked for refinement gets both halves of its root interval in N_1; a
+// record with z integrals awaiting refinement gets its root in RT_0. One
+// block compacts 1024 slots (16 chunks; 4 consecutive slots per thread) in
+// slot order with one atomic per list per block.
+constexpr int kGatherSlots = 1024;
+__global__ __launch_bounds__(256) void gather_kernel(int64_t nw, Work W) {
+  __shared__ int sc[2][256];
+  __shared__ int base[2];
+  const int tid = threadIdx.x;
+  const int64_t s0 = (int64_t)blockIdx.x * kGatherSlots + 4 * tid;
+  int kind[4];  // 0: none, 1: N_1 (2 entries), 2: RT_0 (1 entry)
+  int n1 = 0, n0 = 0;
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
+  for (int q = 0; q < 4; ++q) {
+    const int64_t slot = s0 + q;
+    kind[q] = 0;
+    const int64_t c = slot >> 6;
+    if (c < nw && (slot & 63) < (W.wl_n[c] & 255)) {
+      kind[q] = W.pend[slot] ? 2 : 1;
+      if (kind[q] == 1) n1 += 2;
+      else n0 += 1;
+    }
   }
-  const int tot = __shfl(v, 63, 64);
-  int base = 0;
-  if (lane == 63 && tot) base = atomicAdd(&W.ntask[1], tot);
-  base = __shfl(base, 63, 64);
-  uint32_t* t1 = W.tasks + task_offset(1, W.nslots);
-  int at = base + v - 2 * nt;
-  for (int k = 0; k < nt; ++k) {
-    const uint32_t slot = (uint32_t)(c * 64 + k);
-    t1[at++] = slot << kBfDepth;
-    t1[at++] = (slot << kBfDepth) | 1u;
+  sc[0][tid] = n1;
+  sc[1][tid] = n0;
+  __syncthreads();
+  // block exclusive scans (Hillis-Steele in LDS)
+  for (int o = 1; o < 256; o <<= 1) {
+    const int a1 = tid >= o ? sc[0][tid - o] : 0, a0 = tid >= o ? sc[1][tid - o] : 0;
+    __syncthreads();
+    sc[0][tid] += a1;
+    sc[1][tid] += a0;
+    __syncthreads();
+  }
+  if (tid == 255) {
+    base[0] = sc[0][255] ? atomicAdd(&W.ntask[1], sc[0][255]) : 0;
+    base[1] = sc[1][255] ? atomicAdd(&W.ntask[kRepairCounter], sc[1][255]) : 0;
+  }
+  __syncthreads();
+  int at1 = base[0] + sc[0][tid] - n1, at0 = base[1] + sc[1][tid] - n0;
+  uint32_t* t1 = W.tasks + node_list(1, W.nslots);
+  uint32_t* r0 = W.tasks + repair_list(0, W.nslots);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t e = (uint32_t)(s0 + q) << kBfDepth;
+    if (kind[q] == 1) {
+      t1[at1++] = e;
+      t1[at1++] = e | 1u;
+    } else if (kind[q] == 2) {
+      r0[at0++] = e;
+    }
   }
 }
 
-// Tree level L (1..kBfDepth) breadth-first: one lane per interval of the
-// level. Evaluates f at the interval's d and e (the reference's
-// adaptiveSimpsonsAux evaluations, integrate.pxi:94-104 / 161-169), stores
-// them in the record, runs the stop test and pushes both halves to level L+1
-// when it asks for refinement (past kBfDepth: the record continues on the
-// per-lane walk in fold_kernel). A near-tie marks the record exact; its other
-// tasks then stop.
+// Appends the wave's flagged entries to list `dst` (length counter *cnt), one
+// atomic per wave; n_each entries per flagged lane: e, e + 1, ...
+__device__ inline void wave_push(bool flag, uint32_t e, int n_each, uint32_t* dst, int* cnt) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long b = __ballot(flag);
+  if (!b) return;
+  int at = 0;
+  if (lane == 0) at = atomicAdd(cnt, n_each * __popcll(b));
+  at = __shfl(at, 0, 64);
+  if (flag) {
+    at += n_each * __popcll(b & lanemask_lt(lane));
+    for (int k = 0; k < n_each; ++k) dst[at + k] = e + (uint32_t)k;
+  }
+}
+
+// Tree levels, breadth-first over all tree records. Node (L, m) of a record
+// is an interval of its adaptive tree (m's bits: left / right turns from the
+// root); its geometry and S come from the reference's recursion over the
+// stored values (tree_node).
+//
+// level_kernel<MODE, L> (L = 1..kBfDepth): one lane per interval of N_L.
+// Evaluates f at the interval's d and e (the adaptiveSimpsonsAux
+// evaluations, integrate.pxi:94-104 / 161-169) and stores them. If a z
+// integral there needs refinement (kAdaptTZ) the interval goes to RT_L;
+// otherwise its stop test runs here and a refinement pushes both halves to
+// N_{L+1} (past kBfDepth: the record continues on the per-lane walk in
+// fold_kernel). A near-tie or ambiguous decision marks the record exact; its
+// other tasks then stop.
+template <int MODE, int L>
+__device__ inline void node_test(const TrialArgs& A, const Work& W, const TreeFn<MODE>& fn,
+                                 const TreeNode& nd, int64_t slot, int m, int depth, int& fl,
+                                 bool& push) {
+  const int64_t ns = W.nslots;
+  const double* F = W.F;
+  auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
+  const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), FV(nd.pos + nd.W / 4), FV(nd.pos + nd.W / 2),
+                       FV(nd.pos + 3 * nd.W / 4), FV(nd.pos + nd.W));
+  const bool refine = simpson_refine(nd.S, s.S2, nd.err, depth - L, fl);
+  if (!(fl & kFlagExact) && refine) {
+    if (L < kBfDepth) push = true;
+    else atomicOr(&W.rflag[slot], (int)kFlagFallback);
+  }
+}
+
 template <int MODE, int L, bool COUNT>
 __global__ __launch_bounds__(256) void level_kernel(TrialArgs A, Work W, int depth) {
   const int nt = W.ntask[L];
-  const uint32_t* tl = W.tasks + task_offset(L, W.nslots);
-  uint32_t* next = L < kBfDepth ? W.tasks + task_offset(L + 1, W.nslots) : nullptr;
+  const uint32_t* tl = W.tasks + node_list(L, W.nslots);
   const int lane = threadIdx.x & 63;
   const int64_t stride = (int64_t)gridDim.x * 256;
   for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); base < nt; base += stride) {
     const int64_t t = base + lane;
-    bool push = false;
-    int64_t slot = 0;
-    int m = 0;
+    bool push = false, rep = false;
+    uint32_t e = 0;
     if (t < nt) {
-      const uint32_t e = tl[t];
-      slot = e >> kBfDepth;
-      m = (int)(e & ((1u << kBfDepth) - 1u));
+      e = tl[t];
+      const int64_t slot = e >> kBfDepth;
+      const int m = (int)(e & ((1u << kBfDepth) - 1u));
       if (!(W.rflag[slot] & (kFlagExact | kFlagFallback))) {
         const int64_t i = (slot >> 6) * 64 + W.wl[slot];
         TreeFn<MODE> fn;
@@ -234,45 +300,93 @@ __global__ __launch_bounds__(256) void level_kernel(TrialArgs A, Work W, int dep
         const double d = (nd.lb + c) / 2., ee = (c + nd.ub) / 2.;
         int fl = 0;
         long long ne = 0;
-        bool rd = false, re = false;
-        double fd = fn(d, A.P, A.K, fl, ne, rd);
-        double fe = 0.0;
-        if (!(fl & kFlagExact)) fe = fn(ee, A.P, A.K, fl, ne, re);
-        // z integrals that need refinement (kAdaptTZ), after both roots
-        if (rd && !(fl & kFlagExact)) fd = fn.full(d, A.P, A.K, fl, ne);
-        if (re && !(fl & kFlagExact)) fe = fn.full(ee, A.P, A.K, fl, ne);
-        if (fl & (kFlagFallback | kFlagErrors)) {
-          atomicOr(&W.rflag[slot], (int)kFlagFallback);
-          fl &= ~kFlagErrors;
-        } else if (!(fl & kFlagExact)) {
-          F[(int64_t)(nd.pos + nd.W / 4) * ns + slot] = fd;
-          F[(int64_t)(nd.pos + 3 * nd.W / 4) * ns + slot] = fe;
-          const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), fd, FV(nd.pos + nd.W / 2), fe,
-                               FV(nd.pos + nd.W));
-          const bool refine = simpson_refine(nd.S, s.S2, nd.err, depth - L, fl);
-          if (!(fl & kFlagExact) && refine) {
-            if (L < kBfDepth) push = true;
-            else atomicOr(&W.rflag[slot], (int)kFlagFallback);
+        unsigned pm = 0u;
+        // the two new points from one evaluation site (one copy of the
+        // 5-wide z root in the code: fewer live registers)
+#pragma unroll 1
+        for (int q = 1; q < 4; q += 2) {
+          const double u = q == 1 ? d : ee;
+          const int pos = nd.pos + q * (nd.W / 4);
+          bool r = false;
+          const double y = fn(u, A.P, A.K, fl, ne, r);
+          if (fl & kFlagExact) break;
+          F[(int64_t)pos * ns + slot] = y;
+          if (r) pm |= 1u << pos;
+        }
+        if (!(fl & kFlagExact)) {
+          if (pm) {
+            atomicOr(&W.pend[slot], pm);
+            rep = true;
+          } else {
+            node_test<MODE, L>(A, W, fn, nd, slot, m, depth, fl, push);
           }
         }
         if (fl & kFlagExact) atomicOr(&W.rflag[slot], (int)kFlagExact);
-        if (fl & kFlagErrors) atomicOr(A.status, fl & kFlagErrors);
         if (COUNT) atomicAdd(&W.rcnt[slot], (int)ne);
       }
     }
-    if (L < kBfDepth) {
-      const unsigned long long b = __ballot(push);
-      if (b) {
-        int nb = 0;
-        if (lane == 0) nb = atomicAdd(&W.ntask[L + 1], 2 * __popcll(b));
-        nb = __shfl(nb, 0, 64);
-        if (push) {
-          const int at = nb + 2 * __popcll(b & lanemask_lt(lane));
-          next[at] = ((uint32_t)slot << kBfDepth) | (uint32_t)(2 * m);
-          next[at + 1] = ((uint32_t)slot << kBfDepth) | (uint32_t)(2 * m + 1);
+    const int mb = (int)(e & ((1u << kBfDepth) - 1u));
+    const uint32_t slot_e = e & ~((1u << kBfDepth) - 1u);
+    if (L < kBfDepth)
+      wave_push(push, slot_e | (uint32_t)(2 * mb), 2,
+                W.tasks + node_list(L < kBfDepth ? L + 1 : 1, W.nslots), &W.ntask[L + 1]);
+    wave_push(rep, e, 1, W.tasks + repair_list(L, W.nslots), &W.ntask[kRepairCounter + L]);
+  }
+}
+
+// repair_kernel<MODE, L> (kAdaptTZ, L = 0..kBfDepth): one lane per interval
+// of RT_L: the complete z integrals at its pending points (the root's five at
+// L = 0, else d and e), then its stop test as in level_kernel. The lanes all
+// run refinement walks, so none idles beside another lane's walk.
+template <int MODE, int L, bool COUNT>
+__global__ __launch_bounds__(256) void repair_kernel(TrialArgs A, Work W, int depth) {
+  const int nt = W.ntask[kRepairCounter + L];
+  const uint32_t* tl = W.tasks + repair_list(L, W.nslots);
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); base < nt; base += stride) {
+    const int64_t t = base + (threadIdx.x & 63);
+    bool push = false;
+    uint32_t e = 0;
+    if (t < nt) {
+      e = tl[t];
+      const int64_t slot = e >> kBfDepth;
+      const int m = (int)(e & ((1u << kBfDepth) - 1u));
+      if (!(W.rflag[slot] & (kFlagExact | kFlagFallback))) {
+        const int64_t i = (slot >> 6) * 64 + W.wl[slot];
+        TreeFn<MODE> fn;
+        fn.setup(A.x[i], A.P, A.K);
+        const int64_t ns = W.nslots;
+        double* F = W.F;
+        auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
+        const TreeNode nd = tree_node(FV, fn.lb, fn.ub, A.K.simps_err, L, m);
+        const unsigned pm = W.pend[slot];
+        const double c = (nd.ub + nd.lb) / 2.;
+        const double d = (nd.lb + c) / 2., ee = (c + nd.ub) / 2.;
+        int fl = 0;
+        long long ne = 0;
+#pragma unroll 1
+        for (int q = (L == 0 ? 0 : 1); q < (L == 0 ? 5 : 4); q += (L == 0 ? 1 : 2)) {
+          const int pos = nd.pos + q * (nd.W / 4);
+          if (!((pm >> pos) & 1u) || (fl & kFlagExact)) continue;
+          const double u = q == 0 ? nd.lb : q == 1 ? d : q == 2 ? c : q == 3 ? ee : nd.ub;
+          ne -= 5;  // the full walk evaluates the root again
+          F[(int64_t)pos * ns + slot] = fn.full(u, A.P, A.K, fl, ne);
         }
+        if (fl & kFlagErrors) {
+          atomicOr(&W.rflag[slot], (int)kFlagFallback);
+          fl &= ~kFlagErrors;
+        } else if (!(fl & kFlagExact)) {
+          node_test<MODE, L>(A, W, fn, nd, slot, m, depth, fl, push);
+        }
+        if (fl & kFlagExact) atomicOr(&W.rflag[slot], (int)kFlagExact);
+        if (COUNT) atomicAdd(&W.rcnt[slot], (int)ne);
       }
     }
+    const int mb = (int)(e & ((1u << kBfDepth) - 1u));
+    const uint32_t slot_e = e & ~((1u << kBfDepth) - 1u);
+    if (L < kBfDepth)
+      wave_push(push, slot_e | (uint32_t)(2 * mb), 2,
+                W.tasks + node_list(L < kBfDepth ? L + 1 : 1, W.nslots), &W.ntask[L + 1]);
   }
 }
 
@@ -342,7 +456,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, 
     ne = wave_sum_ll(ne);
     if (lane == 0) atomicAdd(A.evals, (unsigned long long)ne);
   }
-  if (blockIdx.x == 0 && lane <= kBfDepth) W.ntask[lane] = 0;
+  if (blockIdx.x == 0 && lane < 16) W.ntask[lane] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -586,7 +700,8 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
     Q = staged ? rows[nj - first] : P[nj];
     double p, f[5];
     int flags = 0;
-    const int oc = fast_level0<MODE>(x[i], Q, K, p, f, ne, flags);
+    unsigned pend;
+    const int oc = fast_level0<MODE>(x[i], Q, K, p, f, ne, flags, pend);
     if (oc == kFinal) lp[i] = node_logp(p, Q, K);
     else defer = true;
   }
@@ -717,18 +832,37 @@ template <int MODE, bool COUNT, int OUT>
 static void run_deferred(const TrialArgs& A, const Work& W, int depth, hipStream_t s) {
   const int64_t nw = (A.n + 63) / 64;
   if (MODE != kDirect && depth > 0) {
-    hipLaunchKernelGGL(gather_kernel, dim3((nw + 255) / 256), dim3(256), 0, s, W.wl_n, nw, W);
+    hipLaunchKernelGGL(gather_kernel, dim3((nw * 64 + kGatherSlots - 1) / kGatherSlots), dim3(256),
+                       0, s, nw, W);
     const int lv = depth < kBfDepth ? depth : kBfDepth;
     const int64_t gl = std::min<int64_t>(WFPT_LEVEL_GRID, (2 * nw * 64 + 255) / 256);
-    if (lv >= 1)
+    const int64_t gr = std::min<int64_t>(WFPT_LEVEL_GRID, (nw * 64 + 255) / 256);
+    constexpr bool TZ = MODE == kAdaptTZ;
+    if (TZ)
+      hipLaunchKernelGGL((repair_kernel<MODE, 0, COUNT>), dim3(gr), dim3(256), 0, s, A, W, depth);
+    if (lv >= 1) {
       hipLaunchKernelGGL((level_kernel<MODE, 1, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
-    if (lv >= 2)
-      hipLaunchKernelGGL((level_kernel<MODE, (kBfDepth >= 2 ? 2 : 1), COUNT>), dim3(gl), dim3(256),
-                         0, s, A, W, depth);
-    if (lv >= 3)
-      hipLaunchKernelGGL((level_kernel<MODE, (kBfDepth >= 3 ? 3 : 1), COUNT>), dim3(gl), dim3(256),
-                         0, s, A, W, depth);
+      if (TZ)
+        hipLaunchKernelGGL((repair_kernel<MODE, 1, COUNT>), dim3(gr), dim3(256), 0, s, A, W,
+                           depth);
+    }
+    if (lv >= 2) {
+      constexpr int L2 = kBfDepth >= 2 ? 2 : 1;
+      hipLaunchKernelGGL((level_kernel<MODE, L2, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
+      if (TZ)
+        hipLaunchKernelGGL((repair_kernel<MODE, L2, COUNT>), dim3(gr), dim3(256), 0, s, A, W,
+                           depth);
+    }
+    if (lv >= 3) {
+      constexpr int L3 = kBfDepth >= 3 ? 3 : 1;
+      hipLaunchKernelGGL((level_kernel<MODE, L3, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
+      if (TZ)
+        hipLaunchKernelGGL((repair_kernel<MODE, L3, COUNT>), dim3(gr), dim3(256), 0, s, A, W,
+                           depth);
+    }
   }
+  // one wave per chunk up to WFPT_FOLD_GRID waves (latency-bound loads of the
+  // records' tree values: many waves in flight)
   const int64_t gf = std::min<int64_t>(WFPT_FOLD_GRID, nw);
   hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(64), 0, s, A, W, nw, depth);
 }

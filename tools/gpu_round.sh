@@ -8,7 +8,7 @@ OUT=gpurun_out/round
 mkdir -p $OUT
 STAGE=${STAGE:-all}
 if [ "$STAGE" = all ] || [ "$STAGE" = tests ]; then
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread \
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 150 --timeout-method thread \
     > $OUT/pytest_gpu.log 2>&1 || { echo "TESTS_FAIL rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
   tail -3 $OUT/pytest_gpu.log
 fi
