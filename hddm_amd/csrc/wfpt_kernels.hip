@@ -267,7 +267,9 @@ __device__ inline void node_test(const TrialArgs& A, const Work& W, const TreeFn
   auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
   const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), FV(nd.pos + nd.W / 4), FV(nd.pos + nd.W / 2),
                        FV(nd.pos + 3 * nd.W / 4), FV(nd.pos + nd.W));
-  const bool refine = simpson_refine(nd.S, s.S2, nd.err, depth - L, fl);
+  // the root's S comes from its own points, which a repair may just have
+  // replaced; deeper intervals' S (the parent's Sleft / Sright) is final
+  const bool refine = simpson_refine(L == 0 ? s.S : nd.S, s.S2, nd.err, depth - L, fl);
   if (!(fl & kFlagExact) && refine) {
     if (L < kBfDepth) push = true;
     else atomicOr(&W.rflag[slot], (int)kFlagFallback);
