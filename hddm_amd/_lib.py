@@ -83,6 +83,10 @@ wfpt_wiener_like_allreduce = _sig("wfpt_wiener_like_allreduce", _I, [_VP, _VP, _
 wfpt_profile_enable = _sig("wfpt_profile_enable", _I, [_VP, _I])
 wfpt_profile_read = _sig("wfpt_profile_read", _I,
                          [_VP, _PD, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I])
+try:  # diagnostics only: A/B runs may load an older library build without it
+    wfpt_profile_lists = _sig("wfpt_profile_lists", _I, [_VP, ctypes.POINTER(_I64), _I])
+except AttributeError:
+    wfpt_profile_lists = None
 wfpt_synchronize = _sig("wfpt_synchronize", _I, [_VP])
 wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
@@ -92,7 +96,7 @@ EXPORTED = [
     "wfpt_wiener_like_host", "wfpt_wiener_like_nodes", "wfpt_pdf_array", "wfpt_full_pdf",
     "wfpt_wiener_like_multi", "wfpt_dmat_cdf_array", "wfpt_comm_unique_id", "wfpt_comm_init",
     "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
-    "wfpt_decode_result",
+    "wfpt_decode_result", "wfpt_profile_lists",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)
@@ -154,6 +158,17 @@ class Context:
         check(wfpt_profile_read(self.handle, ctypes.byref(ms), ctypes.byref(nl),
                                 ctypes.byref(ne), 1 if reset else 0))
         return ms.value, nl.value, ne.value
+
+    def profile_lists(self, reset=False):
+        """Deferred-pass list sizes (include/wfpt_amd.h: wfpt_profile_lists)."""
+        a = (_I64 * 16)()
+        if wfpt_profile_lists is None:
+            return {}
+        check(wfpt_profile_lists(self.handle, a, 1 if reset else 0))
+        v = list(a)
+        return {"tasks1": v[1], "tasks2": v[2], "records": v[4], "exact": v[5],
+                "walk": v[6], "zwalks": v[7], "zwalks0": v[8], "zwalks1": v[9],
+                "zwalks2": v[10], "phase_kcycles": v[11:16]}
 
     def synchronize(self):
         check(wfpt_synchronize(self.handle))

@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libwfpt_amd.so")
 SOURCES = ["wfpt_kernels.hip", "cdfdif_kernels.hip", "wfpt_capi.cpp"]
-DEPS = SOURCES + ["wfpt_device.hpp", "wfpt_internal.h"]
+DEPS = SOURCES + ["wfpt_device.hpp", "wfpt_internal.h", "wfpt_crlibm.hpp", "wfpt_exact.hpp"]
 ARCH = os.environ.get("WFPT_OFFLOAD_ARCH", "gfx950")
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

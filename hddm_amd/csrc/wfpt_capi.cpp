@@ -107,13 +107,9 @@ struct wfpt_ctx {
   // deferred-trial state of adaptive calls (wfpt_internal.h: Work), sized for
   // the largest call so far: slot-indexed, nslots = 64 * chunks
   DevBuf<unsigned char> wl;  // lane of the deferred trial in each slot
-  DevBuf<int> wl_n;          // per chunk: #tree | #exact << 8
-  DevBuf<int> rflag;         // per slot: kFlag*
-  DevBuf<unsigned> pend;     // per slot: tree points awaiting z refinement
-  DevBuf<double> tf;         // per slot: tree sample values (SoA)
-  DevBuf<int> rcnt;          // per slot: evaluation counts (PROF_EVALS only)
-  DevBuf<uint32_t> tasks;    // tree-level task lists
-  int* ntask = nullptr;      // device: 16 list lengths (0 at rest)
+  DevBuf<int> wl_n;          // per chunk: deferred trials
+  DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
+  int* prof = nullptr;       // device: 16 deferred-pass work counters (PROF_EVALS)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
@@ -219,18 +215,10 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   HIP_TRY(c->wl.reserve(ns));
   HIP_TRY(c->wl_n.reserve(nw));
   HIP_TRY(c->rflag.reserve(ns));
-  HIP_TRY(c->pend.reserve(ns));
-  HIP_TRY(c->tf.reserve(ns * wfpt::kTreePoints));
-  HIP_TRY(c->tasks.reserve(wfpt::task_capacity(ns)));
-  if (c->count) HIP_TRY(c->rcnt.reserve(ns));
   W->wl = c->wl.p;
   W->wl_n = c->wl_n.p;
   W->rflag = c->rflag.p;
-  W->pend = c->pend.p;
-  W->F = c->tf.p;
-  W->rcnt = c->count ? c->rcnt.p : nullptr;
-  W->tasks = c->tasks.p;
-  W->ntask = c->ntask;
+  W->prof = c->prof;
   W->nslots = ns;
   return WFPT_OK;
 }
@@ -420,8 +408,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
-  if (e == hipSuccess) e = hipMalloc((void**)&c->ntask, 16 * sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->ntask, 0, 16 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->prof, 16 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->prof, 0, 16 * sizeof(int));
   if (e == hipSuccess) std::memset(c->mres, 0, 5 * sizeof(double));
   if (e != hipSuccess) {
     wfpt_close(c);
@@ -447,11 +435,7 @@ void wfpt_close(wfpt_ctx* c) {
   c->wl.release();
   c->wl_n.release();
   c->rflag.release();
-  c->pend.release();
-  c->tf.release();
-  c->rcnt.release();
-  c->tasks.release();
-  if (c->ntask) (void)hipFree(c->ntask);
+  if (c->prof) (void)hipFree(c->prof);
   c->defer.release();
   c->nd_idx.release();
   c->nd_par.release();
@@ -824,6 +808,18 @@ int wfpt_profile_read(wfpt_ctx* c, double* kernel_ms, int64_t* launches, int64_t
     c->launches = 0;
     c->n_evals = 0;
   }
+  return WFPT_OK;
+}
+
+int wfpt_profile_lists(wfpt_ctx* c, int64_t counts[16], int reset) {
+  if (!c || !counts) return fail(WFPT_ERR_ARG, "null pointer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  int h[16];
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipMemcpy(h, c->prof, sizeof(h), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 16; ++k) counts[k] = h[k];
+  if (reset) HIP_TRY(hipMemset(c->prof, 0, sizeof(h)));
   return WFPT_OK;
 }
 

@@ -10,10 +10,10 @@
 //   * work that depends only on the non-decision time node t (the series
 //     branch and K, sqrt/log terms, sv normalisers) is hoisted out of the z
 //     integral: one `TNode` per t node serves all z nodes;
-//   * the root level of every adaptive Simpson runs in the level-0 pass
-//     (fast_level0); deeper tree levels run breadth-first over all deferred
-//     trials (TreeFn / tree_node / tree_value, wfpt_kernels.hip), beyond
-//     kBfDepth on a per-lane walk with an explicit stack (adaptive_walk).
+//   * adaptive trees up to kTreeDepth levels per axis complete inside the
+//     wave that owns the trial (engine_kernel, wfpt_kernels.hip: tree_node /
+//     tree_value over the dyadic points); deeper trees continue on a
+//     per-lane walk with an explicit stack (adaptive_walk).
 // Compiled with -ffp-contract=off: no FMA contraction, like the x86-64 build
 // of the reference.
 #pragma once
@@ -941,39 +941,18 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 }
 
 // ---------------------------------------------------------------------------
-// Level-0 pass and breadth-first tree levels (adaptive modes).
+// Adaptive trees (the reference's adaptiveSimpsonsAux recursion) over the
+// dyadic points of the root interval.
 //
 // Node order used below: lb, d, c, e, ub of an interval (integrate.pxi:114-141
-// prologue nodes lb, c, ub + the root aux nodes d, e).
-
-// A deferred trial keeps its tree's sample values at the dyadic points of the
-// root interval, kTreeW + 1 of them, in a slot-indexed structure-of-arrays
-// F[point * nslots + slot]; levels 1..kBfDepth are evaluated breadth-first
-// over all deferred trials (wfpt_kernels.hip: level_kernel). Deeper trees
-// continue on the per-lane walk (kFlagFallback).
-#ifndef WFPT_BF_DEPTH
-#define WFPT_BF_DEPTH 2
-#endif
-constexpr int kBfDepth = WFPT_BF_DEPTH;
-constexpr int kTreeW = 4 << kBfDepth;
+// prologue nodes lb, c, ub + the root aux nodes d, e). The level-0 engine
+// (wfpt_kernels.hip: engine_kernel) completes trees of up to kTreeDepth
+// refinement levels per axis in-wave (HDDM's n_st = n_sz = 2 default); deeper
+// trees continue on the per-lane walk (kFlagFallback). A tree's values live at
+// the kTreePoints dyadic points P_0..P_kTreeW of its root interval.
+constexpr int kTreeDepth = 2;
+constexpr int kTreeW = 4 << kTreeDepth;
 constexpr int kTreePoints = kTreeW + 1;
-
-// Task lists of the breadth-first levels, back to back: node lists N_L
-// (L = 1..kBfDepth: intervals to evaluate, up to 2^L per slot) then
-// repair lists RT_L (L = 0..kBfDepth: intervals whose z integrals need
-// refinement before their stop test, up to 2^L per slot). An entry is
-// slot << kBfDepth | m (m: the interval's index within its level).
-__host__ __device__ inline int64_t node_list(int L, int64_t nslots) {
-  return ((int64_t(1) << L) - 2) * nslots;
-}
-__host__ __device__ inline int64_t repair_list(int L, int64_t nslots) {
-  return ((int64_t(1) << (kBfDepth + 1)) - 2 + (int64_t(1) << L) - 1) * nslots;
-}
-__host__ __device__ inline int64_t task_capacity(int64_t nslots) {
-  return ((int64_t(1) << (kBfDepth + 2)) - 3) * nslots;
-}
-// task counters (Work::ntask): N_L at [L], RT_L at [8 + L]
-constexpr int kRepairCounter = 8;
 
 enum Outcome : int { kFinal = 0, kTree = 1, kExact = 2 };
 
@@ -993,8 +972,7 @@ __device__ inline Simp simp5(double h, double fb, double fd, double fm, double f
 // The z integral at one t node (adaptiveSimpsons_1D over z, integrate.pxi:
 // 114-141), root level only: the root's 5 evaluations 5-wide on the grid and
 // its stop test. repair = the test asks for refinement (the value is then the
-// root estimate; the caller recomputes the node with inner_full after its
-// main loop, where few registers are live).
+// root estimate; the caller defers the trial).
 __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, double v,
                                     double sv, double a, const Knobs& K, int& flags,
                                     long long& ne, bool& repair) {
@@ -1006,19 +984,6 @@ __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, 
   const Simp s = simp5(G.g[4] - G.g[0], f[0], f[1], f[2], f[3], f[4]);
   repair = simpson_refine(s.S, s.S2, K.simps_err, K.n_sz, flags);
   return s.S2 + (s.S2 - s.S) / 15;
-}
-
-// The complete z integral at one t node (root + refinement): a per-lane walk
-// (the repair kernels run it with a scratch stack, any n_sz <= WFPT_MAX_DEPTH).
-template <class Stack>
-__device__ inline double inner_full(const TNode& T, double lbz, double ubz, double iZz, double v,
-                                    double sv, double a, const Knobs& K, int& flags,
-                                    long long& ne) {
-  auto g = [&](double zc) -> double {
-    ++ne;
-    return tnode_pdf_sv(T, zc, v, sv, a) * iZz;
-  };
-  return adaptive_walk<Stack>(g, lbz, ubz, K.simps_err, K.n_sz, flags, ne);
 }
 
 // Root interval of the adaptive tree: over t for kAdaptT / kAdaptTZ, over z
@@ -1034,14 +999,14 @@ __device__ inline void tree_root(const Trial& tr, const Params& P, double& lb, d
   }
 }
 
-// Level-0 pass of one trial for an adaptive (or direct) MODE: the reference's
-// prologue + root aux node of every adaptive Simpson it runs (1, 5, 5 or 25
-// pdf_sv evaluations, + refinements of the z integrals in kAdaptTZ).
+// Level-0 pass of one trial for an adaptive (or direct) MODE, one trial per
+// lane (the direct family and the per-node path): the reference's prologue +
+// root aux node of every adaptive Simpson it runs (1, 5, 5 or 25 pdf_sv
+// evaluations).
 //   kFinal: p is the trial density (0 for invalid parameters);
 //   kTree:  the root stop test asks for refinement, or (kAdaptTZ) some t
-//           node's z integral needs refinement first (bit k of `pend`: tree
-//           point k * kTreeW / 4; the root test then runs after the repair
-//           pass); f[] = the root interval's values at lb, d, c, e, ub;
+//           node's z integral needs refinement (bit k of `pend`: tree point
+//           k * kTreeW / 4); f[] = the root interval's values at lb, d, c, e, ub;
 //   kExact: the value hinges on last-bit rounding (recomputed exactly).
 template <int MODE>
 __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, double& p,
@@ -1148,55 +1113,6 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
   return (p > kExactBelow || structural) ? kFinal : kExact;
 }
 
-// Per-trial state of the tree function f(u) for the level kernels.
-template <int MODE>
-struct TreeFn {
-  Trial tr;
-  double lb, ub, iw;
-  double lbz, ubz, iZz;  // kAdaptTZ: the z range and 1 / (ub_z - lb_z)
-  ZGrid G;               // kAdaptTZ: root z grid
-  TNode T0;              // kAdaptZ: the trial's single t node
-  __device__ inline void setup(double x0, const Params& P, const Knobs& K) {
-    tr = trial_setup(x0, P);
-    tree_root<MODE>(tr, P, lb, ub);
-    iw = 1.0 / (ub - lb);
-    if (MODE == kAdaptTZ) {
-      lbz = tr.z - tr.sz / 2.;
-      ubz = tr.z + tr.sz / 2.;
-      iZz = 1.0 / (ubz - lbz);
-      G = zgrid_setup(lbz, ubz, tr.v, P.sv, P.a);
-    }
-    if (MODE == kAdaptZ) T0 = tnode_setup(tr.x - P.t, tr.v, P.sv, P.a, K.err);
-  }
-  // f(u) of the tree: pdf_sv(x - u, z) / st (T), pdf_sv(x - t, u) / sz (Z),
-  // [z integral at t node u] / st (TZ; root level only, repair = it needs
-  // refinement: then call full(u))
-  __device__ inline double operator()(double u, const Params& P, const Knobs& K, int& flags,
-                                      long long& ne, bool& repair) const {
-    repair = false;
-    if (MODE == kAdaptZ) {
-      if (T0.amb) flags |= kFlagExact;
-      ne += 1;
-      return tnode_pdf_sv(T0, u, tr.v, P.sv, P.a) * iw;
-    }
-    const TNode T = tnode_setup(tr.x - u, tr.v, P.sv, P.a, K.err);
-    if (T.amb) flags |= kFlagExact;
-    if (MODE == kAdaptT) {
-      ne += 1;
-      return tnode_pdf_sv(T, tr.z, tr.v, P.sv, P.a) * iw;
-    }
-    return inner_root(T, G, iZz, tr.v, P.sv, P.a, K, flags, ne, repair) * iw;
-  }
-  // kAdaptTZ: the complete z integral at t node u (repair kernels)
-  __device__ inline double full(double u, const Params& P, const Knobs& K, int& flags,
-                                long long& ne) const {
-    const TNode T = tnode_setup(tr.x - u, tr.v, P.sv, P.a, K.err);
-    if (T.amb) flags |= kFlagExact;
-    return inner_full<MemStack<WFPT_MAX_DEPTH>>(T, lbz, ubz, iZz, tr.v, P.sv, P.a, K, flags, ne) *
-           iw;
-  }
-};
-
 // Geometry of tree node (L, m) (m's bits = left/right turns from the root),
 // computed as the reference's recursion does: bounds by the midpoint
 // (ub + lb) / 2 of each parent, S = the parent's Sleft / Sright, err halved
@@ -1235,29 +1151,35 @@ __device__ inline TreeNode tree_node(FV&& F, double lb0, double ub0, double err0
 
 // The trial's integral from a completed tree: the reference's recursion
 // (leaf S2 + (S2 - S) / 15, internal left + right) re-walked over the stored
-// values; every stop test repeats the level kernels' arithmetic, so it takes
-// the same branch. Only called for trees within kBfDepth.
+// values; every stop test repeats the engine's arithmetic, so it takes the
+// same branch. flags gets kFlagExact for a near-tie and kFlagFallback when an
+// interval at depth kTreeDepth still asks for refinement (the tree is deeper
+// than the stored points); nref = refined intervals (each adds 2 nodes x 2
+// evaluations).
 template <class FV>
-__device__ inline double tree_value(FV&& F, double lb0, double ub0, double err0, int depth) {
+__device__ inline double tree_value(FV&& F, double lb0, double ub0, double err0, int depth,
+                                    int& flags, int& nref) {
   struct Fr {
     double lb, ub, S, err, left;
     int pos, W;
   };
-  Fr stk[kBfDepth > 0 ? kBfDepth : 1];
+  Fr stk[kTreeDepth];
   unsigned right_mask = 0u;
   int sp = 0, bottom = depth;
   double lb = lb0, ub = ub0, err = err0;
   int pos = 0, W = kTreeW;
   double S = simp5(ub0 - lb0, F(0), 0.0, F(kTreeW / 2), 0.0, F(kTreeW)).S;
+  nref = 0;
   for (;;) {
     const Simp s = simp5(ub - lb, F(pos), F(pos + W / 4), F(pos + W / 2), F(pos + 3 * W / 4),
                          F(pos + W));
-    int fl = 0;
-    const bool refine = simpson_refine(S, s.S2, err, bottom, fl);
-    if (refine && sp < kBfDepth) {
+    const bool refine = simpson_refine(S, s.S2, err, bottom, flags);
+    if (refine && sp >= kTreeDepth) flags |= kFlagFallback;
+    if (refine && sp < kTreeDepth) {
+      ++nref;
       const double c = (ub + lb) / 2.;
 #pragma unroll
-      for (int k = 0; k < (kBfDepth > 0 ? kBfDepth : 1); ++k)
+      for (int k = 0; k < kTreeDepth; ++k)
         if (k == sp) stk[k] = Fr{c, ub, s.Sr, err / 2, 0.0, pos + W / 2, W / 2};
       ++sp;
       ub = c;
@@ -1277,11 +1199,11 @@ __device__ inline double tree_value(FV&& F, double lb0, double ub0, double err0,
       const int top = sp - 1;
       Fr fr = stk[0];
 #pragma unroll
-      for (int k = 1; k < (kBfDepth > 0 ? kBfDepth : 1); ++k)
+      for (int k = 1; k < kTreeDepth; ++k)
         if (k == top) fr = stk[k];
       if (!((right_mask >> top) & 1u)) {
 #pragma unroll
-        for (int k = 0; k < (kBfDepth > 0 ? kBfDepth : 1); ++k)
+        for (int k = 0; k < kTreeDepth; ++k)
           if (k == top) stk[k].left = val;
         right_mask |= 1u << top;
         lb = fr.lb;
@@ -1299,6 +1221,60 @@ __device__ inline double tree_value(FV&& F, double lb0, double ub0, double err0,
     }
     if (done) return val;
   }
+}
+
+// z grids of the engine, relative to the dyadic points P of [lb_z, ub_z]:
+// kGridRoot {P0, P4, P8, P12, P16} (the root interval's lb, d, c, e, ub),
+// kGridL1 {P2, P6, P10, P14, +1 unused} (the aux nodes of both halves),
+// kGridL2L {P1, P3, P5, P7, P9}, kGridL2R {P7, P9, P11, P13, P15} (the aux
+// nodes of the four quarters; P7 is taken from L2L, P9 from L2R). Five
+// equally spaced points each, so tnode_pdf_sv_grid5 serves all four.
+enum GridSel : int { kGridRoot = 0, kGridL1 = 1, kGridL2L = 2, kGridL2R = 3 };
+// Dyadic point P_k (k = 0..kTreeW) of [lb, ub] as the reference's recursion
+// computes it: every interval's midpoint is (ub + lb) / 2 of its own bounds
+// and its aux nodes (lb + c) / 2, (c + ub) / 2 (integrate.pxi:94-104) are its
+// children's midpoints, so P_k is the end of the chain of midpoints that
+// bisects down to k (IEEE addition is commutative: operand order is moot).
+__host__ __device__ inline double dyadic_point(double lb, double ub, int k) {
+  if (k <= 0) return lb;
+  if (k >= kTreeW) return ub;
+  int lo = 0, hi = kTreeW;
+  for (;;) {
+    const int mid = (lo + hi) >> 1;
+    const double c = (ub + lb) / 2.;
+    if (k == mid) return c;
+    if (k < mid) {
+      hi = mid;
+      ub = c;
+    } else {
+      lo = mid;
+      lb = c;
+    }
+  }
+}
+
+__device__ inline ZGrid zgrid_of(double lb, double ub, int sel, double v, double sv, double a) {
+  ZGrid G;
+  const int k0 = sel == kGridRoot ? 0 : sel == kGridL1 ? 2 : sel == kGridL2L ? 1 : 7;
+  const int dk = sel == kGridRoot ? 4 : sel == kGridL1 ? 4 : 2;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) G.g[i] = dyadic_point(lb, ub, k0 + i * dk);
+  // the unused fifth node of kGridL1 (P18, past ub <= 1 by sz / 8): any
+  // finite coordinate of the same spacing
+  if (sel == kGridL1) G.g[4] = G.g[3] + (G.g[3] - G.g[2]);
+  sincospi01(G.g[0], G.s0, G.c0);
+  sincospi01(G.g[4], G.s4, G.c4);
+  sincospi01((G.g[4] - G.g[0]) * 0.25, G.sd, G.cd);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    if (sv == 0) {
+      G.A[i] = ((-v) * a) * G.g[i];
+    } else {
+      const double azsv = (a * G.g[i]) * sv;
+      G.A[i] = (azsv * azsv) - (((2.0 * a) * v) * G.g[i]);
+    }
+  }
+  return G;
 }
 
 // P(hit upper boundary), pdf.pxi:67-72

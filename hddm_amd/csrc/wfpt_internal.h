@@ -13,20 +13,18 @@ namespace wfpt {
 struct Params;
 struct Knobs;
 
-// Deferred-trial state of one adaptive call, slot-indexed (slot = chunk * 64 +
-// rank of the trial among its chunk's deferred trials; nslots = chunks * 64).
+// Deferred-trial state of one call, slot-indexed (slot = chunk * 64 + rank
+// of the trial among its chunk's deferred trials; nslots = chunks * 64). The
+// deferred trials are the rare ones the level-0 engine hands on: the exact
+// path (near-ties, ambiguous series decisions, subnormal densities) and trees
+// deeper than its in-wave levels.
 struct Work {
   unsigned char* wl;  // [nslots] lane of the trial in slot
-  int* wl_n;          // [chunks] #tree | #exact << 8 deferred trials of the chunk
-  int* rflag;         // [nslots] kFlag* of the trial in slot
-  unsigned* pend;     // [nslots] tree points whose z integral awaits refinement
-  double* F;          // [kTreePoints * nslots] tree sample values (SoA)
-  int* rcnt;          // [nslots] pdf_sv evaluations so far (evaluation counting only)
-  uint32_t* tasks;    // [task_capacity(nslots)] node and repair lists
-  int* ntask;         // [16] list lengths (0 at rest)
+  int* wl_n;          // [chunks] deferred trials of the chunk
+  int* rflag;         // [nslots] kFlagExact | kFlagFallback of the trial in slot
+  int* prof;          // [16] deferred-pass work counters (evaluation counting only)
   int64_t nslots;
 };
-// node_list / repair_list / task_capacity / kTreePoints: wfpt_device.hpp
 
 // Error flags encoded as counts in one double that survives an RCCL sum:
 // (#ranks with a depth error) + kBudgetUnit * (#ranks with a budget error).
@@ -43,8 +41,8 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 
 // out_kind: 0 = partial {sum, zeros}; 1 = per-trial density (logp => log);
 // 2 = per-trial log p. part: kPassFast (level-0 pass, or the whole fixed
-// Simpson kernel) | kPassDeferred (tree levels + fold). fast_done (optional)
-// is recorded right after the level-0 / trial kernel.
+// Simpson kernel) | kPassDeferred (the deferred trials + fold). fast_done
+// (optional) is recorded right after the engine / trial kernel.
 constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3;
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,

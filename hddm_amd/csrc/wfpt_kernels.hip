@@ -52,10 +52,7 @@ struct FastWaves {
 #ifndef WFPT_SLOW_WAVES
 #define WFPT_SLOW_WAVES 2
 #endif
-// Blocks of the grid-stride deferred-trial kernels (level and fold).
-#ifndef WFPT_LEVEL_GRID
-#define WFPT_LEVEL_GRID 2048
-#endif
+// Blocks of the deferred-trial kernel (fold).
 #ifndef WFPT_FOLD_GRID
 #define WFPT_FOLD_GRID 16384
 #endif
@@ -125,18 +122,30 @@ __device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp,
 }
 
 // ---------------------------------------------------------------------------
-// Level-0 pass. One wave = one chunk of 64 consecutive trials c*64 + lane.
-// Deferred trials of chunk c take slots c*64 + k (k = their rank among the
-// chunk's tree trials, then among its exact trials), so the deferred state is
-// slot-indexed without any atomic.
+// Deferred trials. A trial the level-0 kernels cannot settle (kFlagExact: its
+// value hinges on last-bit rounding; kFlagFallback: its tree is deeper than
+// kTreeDepth) takes slot c * 64 + k of its chunk c (k = its rank among the
+// chunk's deferred trials): no atomic, and fold_kernel finds a chunk's
+// deferred trials on its first lanes.
+__device__ inline void defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag) {
+  const unsigned long long b = __ballot(defer);
+  if (defer) {
+    const int64_t slot = c * 64 + __popcll(b & lanemask_lt(lane));
+    W.wl[slot] = (unsigned char)lane;
+    W.rflag[slot] = rflag;
+  }
+  if (lane == 0) W.wl_n[c] = __popcll(b);
+}
+
+// Direct family (sz = st = 0): one pdf_sv per trial, one chunk of 64 trials
+// per wave.
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void fast_kernel(TrialArgs A, Work W) {
-  // ascending |rt| in dispatch order: the costlier short-RT chunks start first
   const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
-  double p = 0.0, f[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  double p = 0.0, f[5];
   long long ne = 0;
   int flags = 0, oc = kFinal;
   unsigned pend = 0u;
@@ -144,23 +153,8 @@ void fast_kernel(TrialArgs A, Work W) {
   double lp = 0.0;
   int zero = 0;
   if (i < A.n && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
-  // tree records first, then exact records
-  const unsigned long long bt = __ballot(oc == kTree), be = __ballot(oc == kExact);
-  const int nt = __popcll(bt);
-  if (oc != kFinal) {
-    const int k = oc == kTree ? __popcll(bt & lanemask_lt(lane))
-                              : nt + __popcll(be & lanemask_lt(lane));
-    const int64_t slot = c * 64 + k;
-    W.wl[slot] = (unsigned char)lane;
-    W.rflag[slot] = oc == kExact ? (int)kFlagExact : 0;
-    if (oc == kTree) {
-      W.pend[slot] = pend;
-#pragma unroll
-      for (int j = 0; j < 5; ++j) W.F[(int64_t)(j * (kTreeW / 4)) * W.nslots + slot] = f[j];
-    }
-    if (COUNT) W.rcnt[slot] = oc == kTree ? (int)ne : 0;
-  }
-  if (lane == 0) W.wl_n[c] = nt | (__popcll(be) << 8);
+  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
+  defer_slots(W, c, lane, oc != kFinal, kFlagExact);
   if (OUT == OUT_SUM) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
@@ -175,232 +169,377 @@ void fast_kernel(TrialArgs A, Work W) {
   }
 }
 
-// Work lists of the tree records after the level-0 pass: a record whose root
-// test asked for refinement gets both halves of its root interval in N_1; a
-// record with z integrals awaiting refinement gets its root in RT_0. One
-// block compacts 1024 slots (16 chunks; 4 consecutive slots per thread) in
-// slot order with one atomic per list per block.
-constexpr int kGatherSlots = 1024;
-__global__ __launch_bounds__(256) void gather_kernel(int64_t nw, Work W) {
-  __shared__ int sc[2][256];
-  __shared__ int base[2];
-  const int tid = threadIdx.x;
-  const int64_t s0 = (int64_t)blockIdx.x * kGatherSlots + 4 * tid;
-  int kind[4];  // 0: none, 1: N_1 (2 entries), 2: RT_0 (1 entry)
-  int n1 = 0, n0 = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t slot = s0 + q;
-    kind[q] = 0;
-    const int64_t c = slot >> 6;
-    if (c < nw && (slot & 63) < (W.wl_n[c] & 255)) {
-      kind[q] = W.pend[slot] ? 2 : 1;
-      if (kind[q] == 1) n1 += 2;
-      else n0 += 1;
-    }
-  }
-  sc[0][tid] = n1;
-  sc[1][tid] = n0;
-  __syncthreads();
-  // block exclusive scans (Hillis-Steele in LDS)
-  for (int o = 1; o < 256; o <<= 1) {
-    const int a1 = tid >= o ? sc[0][tid - o] : 0, a0 = tid >= o ? sc[1][tid - o] : 0;
-    __syncthreads();
-    sc[0][tid] += a1;
-    sc[1][tid] += a0;
-    __syncthreads();
-  }
-  if (tid == 255) {
-    base[0] = sc[0][255] ? atomicAdd(&W.ntask[1], sc[0][255]) : 0;
-    base[1] = sc[1][255] ? atomicAdd(&W.ntask[kRepairCounter], sc[1][255]) : 0;
-  }
-  __syncthreads();
-  int at1 = base[0] + sc[0][tid] - n1, at0 = base[1] + sc[1][tid] - n0;
-  uint32_t* t1 = W.tasks + node_list(1, W.nslots);
-  uint32_t* r0 = W.tasks + repair_list(0, W.nslots);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const uint32_t e = (uint32_t)(s0 + q) << kBfDepth;
-    if (kind[q] == 1) {
-      t1[at1++] = e;
-      t1[at1++] = e | 1u;
-    } else if (kind[q] == 2) {
-      r0[at0++] = e;
-    }
-  }
+// ---------------------------------------------------------------------------
+// The engine of the adaptive families (kAdaptT, kAdaptZ, kAdaptTZ;
+// integrate.pxi:72-206 driven by pdf.pxi:132-146). One wave owns a chunk of 64
+// consecutive trials and completes their quadrature trees, up to kTreeDepth
+// refinement levels per axis (HDDM's n_st = n_sz = 2), without leaving the
+// wave:
+//   * a task is one evaluation of a trial's integrand at one t node: a 5-wide
+//     z grid (kAdaptZ, kAdaptTZ: tnode_pdf_sv_grid5) or one pdf_sv (kAdaptT).
+//     Level 0 is each lane's own root interval (its 5 t nodes, or its root z
+//     grid). The stop tests of level L (each lane its own tree, in the
+//     reference's order and arithmetic) queue level L + 1's tasks in LDS;
+//     rounds of 64 tasks spread them over the wave's lanes, so the cost of a
+//     level is ceil(tasks / 64) rounds and a chunk with few refining trials
+//     pays few rounds;
+//   * kAdaptTZ: a t node whose z integral asks for refinement queues a z walk:
+//     4 lanes evaluate its 4 z grids (the root again, L1, L2L, L2R: every z
+//     node a depth-2 walk can reach, 16 walks per round), then one lane walks
+//     the z tree over those 17 values (tree_value), in the reference's order;
+//   * every evaluation goes through one code site (the loop of rounds), so the
+//     series code is instantiated once.
+// Data in LDS per wave: the trees' values F[point * 64 + owner lane], the z
+// walks' values, the task queues, the owners' x and flags; per block: the z
+// grids of both boundaries and the t tree's dyadic points.
+// Trials whose value hinges on last-bit rounding (kFlagExact) or whose tree is
+// deeper (kFlagFallback) become deferred slots for fold_kernel.
+constexpr int kEngBlock = 256;
+constexpr int kEngWaves = kEngBlock / 64;
+constexpr int kZBatch = 16;                             // z walks per round
+constexpr int kQCap = 2 * (1 << kTreeDepth) * 64;      // tasks of one level
+constexpr int kFlagIdle = 16;                           // lane without a trial to integrate
+constexpr int kFlagStop = kFlagExact | kFlagFallback | kFlagIdle;
+
+struct EngWave {
+  double F[kTreePoints * 64];       // tree values: point * 64 + owner
+  double ZV[kZBatch * kTreePoints];  // the current round's z walks
+  double X[64];                      // the owners' x
+  ZGrid G[2][4];                     // [x > 0][GridSel]: z grids of each boundary's root z interval
+  double tc[kTreePoints];            // the t tree's dyadic points
+  double lbz[2], ubz[2], hz[2], iz[2];  // per boundary: z interval, width, 1 / width
+  int fl[64];                        // the owners' flags
+  int cnt[64];                       // the owners' pdf_sv evaluations (COUNT)
+  uint16_t Q[kQCap];                 // tasks of the current level: owner | point << 6 | grid << 11
+  uint16_t ZQ[kQCap];                // z walks of the current level: owner | point << 6
+};
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Appends the wave's flagged entries to list `dst` (length counter *cnt), one
-// atomic per wave; n_each entries per flagged lane: e, e + 1, ...
-__device__ inline void wave_push(bool flag, uint32_t e, int n_each, uint32_t* dst, int* cnt) {
+// Appends `code` of every flagged lane to q[base...] in lane order; returns
+// the new length (wave-uniform).
+__device__ inline int wave_append(bool flag, int code, uint16_t* q, int base) {
   const int lane = threadIdx.x & 63;
   const unsigned long long b = __ballot(flag);
-  if (!b) return;
-  int at = 0;
-  if (lane == 0) at = atomicAdd(cnt, n_each * __popcll(b));
-  at = __shfl(at, 0, 64);
-  if (flag) {
-    at += n_each * __popcll(b & lanemask_lt(lane));
-    for (int k = 0; k < n_each; ++k) dst[at + k] = e + (uint32_t)k;
-  }
+  if (flag) q[base + __popcll(b & lanemask_lt(lane))] = (uint16_t)code;
+  return base + __popcll(b);
 }
 
-// Tree levels, breadth-first over all tree records. Node (L, m) of a record
-// is an interval of its adaptive tree (m's bits: left / right turns from the
-// root); its geometry and S come from the reference's recursion over the
-// stored values (tree_node).
-//
-// level_kernel<MODE, L> (L = 1..kBfDepth): one lane per interval of N_L.
-// Evaluates f at the interval's d and e (the adaptiveSimpsonsAux
-// evaluations, integrate.pxi:94-104 / 161-169) and stores them. If a z
-// integral there needs refinement (kAdaptTZ) the interval goes to RT_L;
-// otherwise its stop test runs here and a refinement pushes both halves to
-// N_{L+1} (past kBfDepth: the record continues on the per-lane walk in
-// fold_kernel). A near-tie or ambiguous decision marks the record exact; its
-// other tasks then stop.
-template <int MODE, int L>
-__device__ inline void node_test(const TrialArgs& A, const Work& W, const TreeFn<MODE>& fn,
-                                 const TreeNode& nd, int64_t slot, int m, int depth, int& fl,
-                                 bool& push) {
-  const int64_t ns = W.nslots;
-  const double* F = W.F;
-  auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
-  const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), FV(nd.pos + nd.W / 4), FV(nd.pos + nd.W / 2),
-                       FV(nd.pos + 3 * nd.W / 4), FV(nd.pos + nd.W));
-  // the root's S comes from its own points, which a repair may just have
-  // replaced; deeper intervals' S (the parent's Sleft / Sright) is final
-  const bool refine = simpson_refine(L == 0 ? s.S : nd.S, s.S2, nd.err, depth - L, fl);
-  if (!(fl & kFlagExact) && refine) {
-    if (L < kBfDepth) push = true;
-    else atomicOr(&W.rflag[slot], (int)kFlagFallback);
-  }
+// Point of value y[j] of a grid (GridSel) and whether this grid supplies it.
+__device__ inline int grid_point(int gs, int j) {
+  const int k0 = gs == kGridRoot ? 0 : gs == kGridL1 ? 2 : gs == kGridL2L ? 1 : 7;
+  return k0 + j * (gs <= kGridL1 ? 4 : 2);
+}
+__device__ inline bool grid_owns(int gs, int j) {
+  return gs == kGridRoot ? true : gs == kGridL2R ? j > 0 : j < 4;
 }
 
-template <int MODE, int L, bool COUNT>
-__global__ __launch_bounds__(256) void level_kernel(TrialArgs A, Work W, int depth) {
-  const int nt = W.ntask[L];
-  const uint32_t* tl = W.tasks + node_list(L, W.nslots);
+// WFPT_PHASE_TIMING (diagnostic builds): shader-clock time per engine phase,
+// summed over waves into W.prof[11..15] in units of 1024 cycles (level 0,
+// tables, z rounds, t rounds, tests + epilogue).
+#ifdef WFPT_PHASE_TIMING
+#define PHASE_MARK(k)                                    \
+  do {                                                   \
+    const long long now_ = __builtin_amdgcn_s_memtime(); \
+    ph[k] += now_ - ph_t;                                \
+    ph_t = now_;                                         \
+  } while (0)
+#else
+#define PHASE_MARK(k) \
+  do {                \
+  } while (0)
+#endif
+
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work W) {
+#ifdef WFPT_PHASE_TIMING
+  long long ph[5] = {0, 0, 0, 0, 0};
+  long long ph_t = __builtin_amdgcn_s_memtime();
+#endif
+  __shared__ EngWave wave_lds[kEngWaves];
   const int lane = threadIdx.x & 63;
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); base < nt; base += stride) {
-    const int64_t t = base + lane;
-    bool push = false, rep = false;
-    uint32_t e = 0;
-    if (t < nt) {
-      e = tl[t];
-      const int64_t slot = e >> kBfDepth;
-      const int m = (int)(e & ((1u << kBfDepth) - 1u));
-      if (!(W.rflag[slot] & (kFlagExact | kFlagFallback))) {
-        const int64_t i = (slot >> 6) * 64 + W.wl[slot];
-        TreeFn<MODE> fn;
-        fn.setup(A.x[i], A.P, A.K);
-        const int64_t ns = W.nslots;
-        double* F = W.F;
-        auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
-        const TreeNode nd = tree_node(FV, fn.lb, fn.ub, A.K.simps_err, L, m);
-        const double c = (nd.ub + nd.lb) / 2.;
-        const double d = (nd.lb + c) / 2., ee = (c + nd.ub) / 2.;
-        int fl = 0;
-        long long ne = 0;
-        unsigned pm = 0u;
-        // the two new points from one evaluation site (one copy of the
-        // 5-wide z root in the code: fewer live registers)
+  EngWave& wv = wave_lds[threadIdx.x >> 6];
+  EngWave& sh = wv;  // per-wave tables: no block barrier anywhere
+  const double v = A.P.v, sv = A.P.sv, a = A.P.a, z = A.P.z, t = A.P.t;
+  const double err = A.K.err, se = A.K.simps_err;
+  const int nsz = A.K.n_sz;
+  const int depth = (MODE == kAdaptZ) ? A.K.n_sz : A.K.n_st;
+  const int64_t i = (int64_t)blockIdx.x * kEngBlock + threadIdx.x;
+  const int64_t c = i >> 6;
+  // (little state lives across level 0: the trial's setup is redone after it)
+  const double* xp = A.x + (i < A.n ? i : 0);
+  // ---- level 0, each lane its own trial, in registers (fast_level0: the
+  // root interval's 5 t nodes with shared series decisions and the q
+  // recurrence, or the root z grid) ----
+  double p = 0.0, f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  long long ne0 = 0;
+  int fl0 = 0, oc = kFinal;
+  unsigned pend0 = 0u;
+  if (i < A.n) oc = fast_level0<MODE>(*xp, A.P, A.K, p, f0, ne0, fl0, pend0);
+  PHASE_MARK(0);
+  const double x0 = i < A.n ? *xp : 0.0;
+  const Trial tr = trial_setup(x0, A.P);
+  double lb, ub;
+  tree_root<MODE>(tr, A.P, lb, ub);
+  const double iw = (MODE == kAdaptZ) ? 0.0 : 1.0 / (ub - lb);
+  wv.X[lane] = x0;
+  wv.fl[lane] = oc == kTree ? 0 : (oc == kExact ? (int)kFlagExact : (int)kFlagIdle);
+  if (COUNT) wv.cnt[lane] = (int)ne0;
+
+  int L = 0, stage = 1, r = 0, nq = 0, nz = 0;
+  unsigned act = 1u;  // own tree: the intervals of level L under test
+  int pq1 = 0, pq2 = 0, prec = 0, pz0 = 0, pz1 = 0, pz2 = 0;  // COUNT: work tallies
+  if (__ballot(oc == kTree)) {
+    // the wave's tables (trial_setup's flip: x > 0 => v = -v, z = 1 - z):
+    // lanes 0..7 one z grid each, lanes 8..24 one t point each
+    if (MODE != kAdaptT && lane < 8) {
+      const int flip = lane >> 2, sel = lane & 3;
+      const double zf = flip ? 1. - z : z, vf = flip ? -v : v;
+      const double zl = zf - A.P.sz / 2., zu = zf + A.P.sz / 2.;
+      sh.G[flip][sel] = zgrid_of(zl, zu, sel, vf, sv, a);
+      if (sel == 0) {
+        sh.lbz[flip] = zl;
+        sh.ubz[flip] = zu;
+        sh.hz[flip] = zu - zl;
+        sh.iz[flip] = 1.0 / (zu - zl);
+      }
+    }
+    if (MODE != kAdaptZ && lane >= 8 && lane < 8 + kTreePoints)
+      sh.tc[lane - 8] = dyadic_point(t - A.P.st / 2., t + A.P.st / 2., lane - 8);
+    // the refining trials' root values (a pending z integral's value comes
+    // from its z walk) and their pending z integrals (kAdaptTZ)
+    if (oc == kTree) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) wv.F[j * (kTreeW / 4) * 64 + lane] = f0[j];
+    }
+    if (MODE == kAdaptTZ) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        nz = wave_append(oc == kTree && ((pend0 >> (j * (kTreeW / 4))) & 1u),
+                         lane | ((j * (kTreeW / 4)) << 6), wv.ZQ, nz);
+    }
+    wave_sync();
+    PHASE_MARK(1);
 #pragma unroll 1
-        for (int q = 1; q < 4; q += 2) {
-          const double u = q == 1 ? d : ee;
-          const int pos = nd.pos + q * (nd.W / 4);
-          bool r = false;
-          const double y = fn(u, A.P, A.K, fl, ne, r);
-          if (fl & kFlagExact) break;
-          F[(int64_t)pos * ns + slot] = y;
-          if (r) pm |= 1u << pos;
+    for (;;) {
+      if (stage == 0 && r * 64 >= nq) {
+        stage = 1;
+        r = 0;
+      }
+      if (stage == 1 && (MODE != kAdaptTZ || r * kZBatch >= nz)) stage = 2;
+      if (stage == 2) {
+        PHASE_MARK(2);  // (the t rounds are marked at their end)
+        if (COUNT) {
+          if (L == 0) pz0 = nz;
+          else if (L == 1) pz1 = nz;
+          else pz2 = nz;
         }
-        if (!(fl & kFlagExact)) {
-          if (pm) {
-            atomicOr(&W.pend[slot], pm);
-            rep = true;
-          } else {
-            node_test<MODE, L>(A, W, fn, nd, slot, m, depth, fl, push);
+        // stop tests of level L, each lane its own tree (adaptiveSimpsonsAux,
+        // integrate.pxi:105 / 170): refined intervals make their children
+        // level L + 1's intervals
+        unsigned nxt = 0u;
+        if (!(wv.fl[lane] & kFlagStop)) {
+          int f = 0;
+          auto FV = [&](int k) -> double { return wv.F[k * 64 + lane]; };
+          for (int m = 0; m < (1 << L); ++m) {
+            if (!((act >> m) & 1u)) continue;
+            const TreeNode nd = tree_node(FV, lb, ub, se, L, m);
+            const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), FV(nd.pos + nd.W / 4),
+                                 FV(nd.pos + nd.W / 2), FV(nd.pos + 3 * nd.W / 4),
+                                 FV(nd.pos + nd.W));
+            if (simpson_refine(nd.S, s.S2, nd.err, depth - L, f)) nxt |= 3u << (2 * m);
+          }
+          if (L == kTreeDepth && nxt) f |= kFlagFallback;  // deeper than the in-wave levels
+          if (f) {
+            wv.fl[lane] |= f;
+            nxt = 0u;
           }
         }
-        if (fl & kFlagExact) atomicOr(&W.rflag[slot], (int)kFlagExact);
-        if (COUNT) atomicAdd(&W.rcnt[slot], (int)ne);
+        if (COUNT && L == 0) prec = __popcll(__ballot(nxt != 0u));
+        if (L == kTreeDepth) break;
+        act = nxt;
+        // level L + 1's tasks, in lane order
+        int n = 0;
+        if (MODE == kAdaptZ) {
+          for (int m = 0; m < (1 << L); ++m)
+            n = wave_append((act >> (2 * m)) & 1u,
+                            lane | ((L == 0 ? kGridL1 : kGridL2L + m) << 11), wv.Q, n);
+        } else {
+          const int wc = kTreeW >> (L + 1);  // width of a level-(L + 1) interval
+          for (int k = 0; k < (2 << L); ++k)
+            for (int q = 1; q < 4; q += 2)
+              n = wave_append((act >> k) & 1u, lane | ((k * wc + q * (wc / 4)) << 6), wv.Q, n);
+        }
+        if (COUNT) {
+          if (L == 0) pq1 = n;
+          else pq2 = n;
+        }
+        nq = n;
+        wave_sync();
+        PHASE_MARK(4);
+        if (nq == 0) break;
+        ++L;
+        stage = 0;
+        r = 0;
+        nz = 0;
+        continue;
       }
+      // ---- one round: at most one evaluation per lane ----
+      int owner = lane, pos = 0, gs = kGridRoot;
+      bool on;
+      if (stage == 0) {
+        const int e = r * 64 + lane;
+        on = e < nq;
+        if (on) {
+          const int code = wv.Q[e];
+          owner = code & 63;
+          pos = (code >> 6) & 31;
+          gs = code >> 11;
+        }
+      } else {
+        const int e = r * kZBatch + (lane >> 2);
+        on = e < nz;
+        gs = lane & 3;
+        if (on) {
+          const int code = wv.ZQ[e];
+          owner = code & 63;
+          pos = (code >> 6) & 31;
+        }
+      }
+      on = on && !(wv.fl[owner] & kFlagStop);
+      double y[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      int flip = 0;
+      if (on) {
+        const double xo = wv.X[owner];
+        flip = xo > 0;
+        const double vo = flip ? -v : v;
+        const double xa = fabs(xo);
+        const double xx = (MODE == kAdaptZ) ? xa - t : xa - sh.tc[pos];
+        const TNode T = tnode_setup(xx, vo, sv, a, err);
+        if (T.amb) atomicOr(&wv.fl[owner], (int)kFlagExact);
+        if (MODE == kAdaptT) y[0] = tnode_pdf_sv(T, flip ? 1. - z : z, vo, sv, a);
+        else tnode_pdf_sv_grid5(T, sh.G[flip][gs], vo, sv, a, y);
+      }
+      if (stage == 0) {
+        bool pend = false;
+        if (on) {
+          if (MODE == kAdaptT) {
+            wv.F[pos * 64 + owner] = y[0] * iw;
+            if (COUNT) atomicAdd(&wv.cnt[owner], 1);
+          } else if (MODE == kAdaptZ) {
+            const double izf = sh.iz[flip];
+#pragma unroll
+            for (int j = 0; j < 5; ++j)
+              if (grid_owns(gs, j)) wv.F[grid_point(gs, j) * 64 + owner] = y[j] * izf;
+            if (COUNT) atomicAdd(&wv.cnt[owner], 4);
+          } else {
+            // kAdaptTZ: the z integral's prologue + root test (integrate.pxi:
+            // 114-141); a refinement queues the z walk
+            const double izf = sh.iz[flip];
+            const Simp s = simp5(sh.hz[flip], y[0] * izf, y[1] * izf, y[2] * izf, y[3] * izf,
+                                 y[4] * izf);
+            int f = 0;
+            pend = simpson_refine(s.S, s.S2, se, nsz, f);
+            if (f) atomicOr(&wv.fl[owner], f);
+            else if (!pend) wv.F[pos * 64 + owner] = (s.S2 + (s.S2 - s.S) / 15) * iw;
+            if (COUNT) atomicAdd(&wv.cnt[owner], 5);
+          }
+        }
+        if (MODE == kAdaptTZ) nz = wave_append(pend && on, owner | (pos << 6), wv.ZQ, nz);
+      } else if (MODE == kAdaptTZ) {
+        if (on) {
+          const double izf = sh.iz[flip];
+          double* zv = wv.ZV + (lane >> 2) * kTreePoints;
+#pragma unroll
+          for (int j = 0; j < 5; ++j)
+            if (grid_owns(gs, j)) zv[grid_point(gs, j)] = y[j] * izf;
+        }
+        wave_sync();
+        const int e = r * kZBatch + lane;
+        if (lane < kZBatch && e < nz) {
+          const int code = wv.ZQ[e];
+          const int ow = code & 63, ps = (code >> 6) & 31;
+          if (!(wv.fl[ow] & kFlagStop)) {
+            const int fz = wv.X[ow] > 0;
+            const double* zv = wv.ZV + lane * kTreePoints;
+            int f = 0, nref = 0;
+            const double zi = tree_value([&](int k) -> double { return zv[k]; }, sh.lbz[fz],
+                                         sh.ubz[fz], se, nsz, f, nref);
+            if (f) atomicOr(&wv.fl[ow], f);
+            else wv.F[ps * 64 + ow] = zi * iw;
+            if (COUNT) atomicAdd(&wv.cnt[ow], 4 * nref);
+          }
+        }
+      }
+      ++r;
+      wave_sync();
+      if (stage == 0) PHASE_MARK(3);
     }
-    const int mb = (int)(e & ((1u << kBfDepth) - 1u));
-    const uint32_t slot_e = e & ~((1u << kBfDepth) - 1u);
-    if (L < kBfDepth)
-      wave_push(push, slot_e | (uint32_t)(2 * mb), 2,
-                W.tasks + node_list(L < kBfDepth ? L + 1 : 1, W.nslots), &W.ntask[L + 1]);
-    wave_push(rep, e, 1, W.tasks + repair_list(L, W.nslots), &W.ntask[kRepairCounter + L]);
+    wave_sync();
   }
-}
-
-// repair_kernel<MODE, L> (kAdaptTZ, L = 0..kBfDepth): one lane per interval
-// of RT_L: the complete z integrals at its pending points (the root's five at
-// L = 0, else d and e), then its stop test as in level_kernel. The lanes all
-// run refinement walks, so none idles beside another lane's walk.
-template <int MODE, int L, bool COUNT>
-__global__ __launch_bounds__(256) void repair_kernel(TrialArgs A, Work W, int depth) {
-  const int nt = W.ntask[kRepairCounter + L];
-  const uint32_t* tl = W.tasks + repair_list(L, W.nslots);
-  const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t base = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); base < nt; base += stride) {
-    const int64_t t = base + (threadIdx.x & 63);
-    bool push = false;
-    uint32_t e = 0;
-    if (t < nt) {
-      e = tl[t];
-      const int64_t slot = e >> kBfDepth;
-      const int m = (int)(e & ((1u << kBfDepth) - 1u));
-      if (!(W.rflag[slot] & (kFlagExact | kFlagFallback))) {
-        const int64_t i = (slot >> 6) * 64 + W.wl[slot];
-        TreeFn<MODE> fn;
-        fn.setup(A.x[i], A.P, A.K);
-        const int64_t ns = W.nslots;
-        double* F = W.F;
-        auto FV = [&](int j) -> double { return F[(int64_t)j * ns + slot]; };
-        const TreeNode nd = tree_node(FV, fn.lb, fn.ub, A.K.simps_err, L, m);
-        const unsigned pm = W.pend[slot];
-        const double c = (nd.ub + nd.lb) / 2.;
-        const double d = (nd.lb + c) / 2., ee = (c + nd.ub) / 2.;
-        int fl = 0;
-        long long ne = 0;
-#pragma unroll 1
-        for (int q = (L == 0 ? 0 : 1); q < (L == 0 ? 5 : 4); q += (L == 0 ? 1 : 2)) {
-          const int pos = nd.pos + q * (nd.W / 4);
-          if (!((pm >> pos) & 1u) || (fl & kFlagExact)) continue;
-          const double u = q == 0 ? nd.lb : q == 1 ? d : q == 2 ? c : q == 3 ? ee : nd.ub;
-          ne -= 5;  // the full walk evaluates the root again
-          F[(int64_t)pos * ns + slot] = fn.full(u, A.P, A.K, fl, ne);
-        }
-        if (fl & kFlagErrors) {
-          atomicOr(&W.rflag[slot], (int)kFlagFallback);
-          fl &= ~kFlagErrors;
-        } else if (!(fl & kFlagExact)) {
-          node_test<MODE, L>(A, W, fn, nd, slot, m, depth, fl, push);
-        }
-        if (fl & kFlagExact) atomicOr(&W.rflag[slot], (int)kFlagExact);
-        if (COUNT) atomicAdd(&W.rcnt[slot], (int)ne);
-      }
+  // ---- the own trial: its density (level 0, or its tree's value: the
+  // reference's recursion over the stored values), or a deferred slot ----
+  bool defer = oc == kExact;
+  int rf = kFlagExact;
+  if (oc == kTree) {
+    const int ff = wv.fl[lane];
+    if (ff & (kFlagExact | kFlagFallback)) {
+      defer = true;
+      rf = (ff & kFlagExact) ? kFlagExact : kFlagFallback;
+    } else {
+      int f = 0, nref = 0;
+      p = tree_value([&](int k) -> double { return wv.F[k * 64 + lane]; }, lb, ub, se, depth, f,
+                     nref);
+      // structural zero: no evaluation point with x - t_node > 0
+      const bool structural = (MODE == kAdaptZ) ? tr.x - t <= 0 : tr.x - lb <= 0;
+      defer = (f & (kFlagExact | kFlagFallback)) || !(p > kExactBelow || structural);
     }
-    const int mb = (int)(e & ((1u << kBfDepth) - 1u));
-    const uint32_t slot_e = e & ~((1u << kBfDepth) - 1u);
-    if (L < kBfDepth)
-      wave_push(push, slot_e | (uint32_t)(2 * mb), 2,
-                W.tasks + node_list(L < kBfDepth ? L + 1 : 1, W.nslots), &W.ntask[L + 1]);
+  }
+  double lp = 0.0;
+  int zero = 0;
+  if (i < A.n && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
+  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
+  defer_slots(W, c, lane, defer, rf);
+  if (OUT == OUT_SUM) {
+    lp = wave_sum(lp);
+    const int zs = __popcll(__ballot(zero != 0));
+    if (lane == 0) {
+      A.out[c] = lp;
+      A.zeros[c] = zs;
+    }
+  }
+#ifdef WFPT_PHASE_TIMING
+  PHASE_MARK(4);
+  if (lane == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&W.prof[11 + k], (int)(ph[k] >> 10));
+#endif
+  if (COUNT) {
+    const long long nf = wave_sum_ll((i < A.n && !defer) ? (long long)wv.cnt[lane] : 0ll);
+    if (lane == 0) {
+      atomicAdd(A.evals, (unsigned long long)nf);
+      // wfpt_profile_lists
+      atomicAdd(&W.prof[1], pq1);
+      atomicAdd(&W.prof[2], pq2);
+      atomicAdd(&W.prof[4], prec);
+      atomicAdd(&W.prof[7], pz0 + pz1 + pz2);
+      atomicAdd(&W.prof[8], pz0);
+      atomicAdd(&W.prof[9], pz1);
+      atomicAdd(&W.prof[10], pz2);
+    }
   }
 }
 
 // Settles every deferred trial and folds it into its chunk: block g walks
 // chunks g, g + G, ... (64 chunk counts per parallel load); a chunk's deferred
-// trials run on its first lanes: tree records re-walk their completed tree,
-// exact records take the exact path, deeper trees the per-lane walk. OUT_SUM:
-// chunk partial += wave sum of the deferred log densities (fixed lane order).
-// Last kernel of the deferred sequence: resets the level counters.
+// trials run on its first lanes (the exact path, or the per-lane walk for
+// deeper trees). OUT_SUM: chunk partial += wave sum of the deferred log
+// densities (fixed lane order).
 template <int MODE, bool COUNT, int OUT>
-__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw,
-                                                                 int depth) {
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw) {
   const int lane = threadIdx.x;
   const int64_t G = gridDim.x;
   long long ne = 0;
@@ -412,8 +551,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, 
     while (work) {
       const int j = __ffsll((long long)work) - 1;
       work &= work - 1;
-      const int wn = __shfl(mycnt, j, 64);
-      const int ntot = (wn & 255) + (wn >> 8);
+      const int ntot = __shfl(mycnt, j, 64);
       const int64_t c = b0 + (int64_t)j * G;
       double lp = 0.0;
       int zero = 0;
@@ -423,25 +561,11 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, 
         const double x = A.x[i];
         const int fl = W.rflag[slot];
         long long n1 = 0;
-        double p;
-        if (fl & kFlagExact) {
-          p = exact_pdf(x, A.P, A.K, &n1, &errf);
-        } else if (fl & kFlagFallback) {
-          p = fallback_pdf<MODE>(x, A.P, A.K, &n1, &errf);
-        } else {
-          const Trial tr = trial_setup(x, A.P);
-          double lb, ub;
-          tree_root<MODE>(tr, A.P, lb, ub);
-          const int64_t ns = W.nslots;
-          const double* F = W.F;
-          p = tree_value([&](int q) -> double { return F[(int64_t)q * ns + slot]; }, lb, ub,
-                         A.K.simps_err, depth);
-          if (COUNT) n1 = W.rcnt[slot];
-          const bool structural = (MODE == kAdaptZ) ? tr.x - A.P.t <= 0 : tr.x - lb <= 0;
-          p = settle(p, x, A.P, A.K, structural, n1, errf);
-        }
+        const double p = (fl & kFlagExact) ? exact_pdf(x, A.P, A.K, &n1, &errf)
+                                           : fallback_pdf<MODE>(x, A.P, A.K, &n1, &errf);
         ne += n1;
         emit<OUT>(A, i, p, lp, zero);
+        if (COUNT) atomicAdd(&W.prof[(fl & kFlagExact) ? 5 : 6], 1);
       }
       if (OUT == OUT_SUM) {
         lp = wave_sum(lp);
@@ -458,7 +582,6 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, 
     ne = wave_sum_ll(ne);
     if (lane == 0) atomicAdd(A.evals, (unsigned long long)ne);
   }
-  if (blockIdx.x == 0 && lane < 16) W.ntask[lane] = 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -825,57 +948,30 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
 
 template <int MODE, bool COUNT, int OUT>
 static void run_fast(const TrialArgs& A, const Work& W, hipStream_t s, hipEvent_t fast_done) {
-  hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock), 0,
-                     s, A, W);
+  if constexpr (MODE == kDirect)
+    hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
+                       0, s, A, W);
+  else
+    hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>), dim3((A.n + kEngBlock - 1) / kEngBlock),
+                       dim3(kEngBlock), 0, s, A, W);
   if (fast_done) (void)hipEventRecord(fast_done, s);
 }
 
 template <int MODE, bool COUNT, int OUT>
-static void run_deferred(const TrialArgs& A, const Work& W, int depth, hipStream_t s) {
+static void run_deferred(const TrialArgs& A, const Work& W, hipStream_t s) {
+  // one wave per chunk up to WFPT_FOLD_GRID waves
   const int64_t nw = (A.n + 63) / 64;
-  if (MODE != kDirect && depth > 0) {
-    hipLaunchKernelGGL(gather_kernel, dim3((nw * 64 + kGatherSlots - 1) / kGatherSlots), dim3(256),
-                       0, s, nw, W);
-    const int lv = depth < kBfDepth ? depth : kBfDepth;
-    const int64_t gl = std::min<int64_t>(WFPT_LEVEL_GRID, (2 * nw * 64 + 255) / 256);
-    const int64_t gr = std::min<int64_t>(WFPT_LEVEL_GRID, (nw * 64 + 255) / 256);
-    constexpr bool TZ = MODE == kAdaptTZ;
-    if (TZ)
-      hipLaunchKernelGGL((repair_kernel<MODE, 0, COUNT>), dim3(gr), dim3(256), 0, s, A, W, depth);
-    if (lv >= 1) {
-      hipLaunchKernelGGL((level_kernel<MODE, 1, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
-      if (TZ)
-        hipLaunchKernelGGL((repair_kernel<MODE, 1, COUNT>), dim3(gr), dim3(256), 0, s, A, W,
-                           depth);
-    }
-    if (lv >= 2) {
-      constexpr int L2 = kBfDepth >= 2 ? 2 : 1;
-      hipLaunchKernelGGL((level_kernel<MODE, L2, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
-      if (TZ)
-        hipLaunchKernelGGL((repair_kernel<MODE, L2, COUNT>), dim3(gr), dim3(256), 0, s, A, W,
-                           depth);
-    }
-    if (lv >= 3) {
-      constexpr int L3 = kBfDepth >= 3 ? 3 : 1;
-      hipLaunchKernelGGL((level_kernel<MODE, L3, COUNT>), dim3(gl), dim3(256), 0, s, A, W, depth);
-      if (TZ)
-        hipLaunchKernelGGL((repair_kernel<MODE, L3, COUNT>), dim3(gr), dim3(256), 0, s, A, W,
-                           depth);
-    }
-  }
-  // one wave per chunk up to WFPT_FOLD_GRID waves (latency-bound loads of the
-  // records' tree values: many waves in flight)
   const int64_t gf = std::min<int64_t>(WFPT_FOLD_GRID, nw);
-  hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(64), 0, s, A, W, nw, depth);
+  hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(64), 0, s, A, W, nw);
 }
 
 template <bool COUNT, int OUT>
-static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, int depth,
+static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W,
                         hipStream_t s, hipEvent_t fast_done) {
 #define FAST_AND_DEFERRED(M_)                                               \
   do {                                                                      \
     if (part & kPassFast) run_fast<M_, COUNT, OUT>(A, W, s, fast_done);     \
-    if (part & kPassDeferred) run_deferred<M_, COUNT, OUT>(A, W, depth, s); \
+    if (part & kPassDeferred) run_deferred<M_, COUNT, OUT>(A, W, s);        \
   } while (0)
   switch (mode) {
     case kDirect: FAST_AND_DEFERRED(kDirect); break;
@@ -899,11 +995,6 @@ static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, i
   if (fast_done && mode > kAdaptTZ) (void)hipEventRecord(fast_done, s);
 }
 
-static int tree_depth(const Params& P, const Knobs& K) {
-  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  return mode == kAdaptZ ? K.n_sz : K.n_st;
-}
-
 bool has_deferred_pass(const Params& P, const Knobs& K) {
   return select_mode(P.sz, P.st, K.use_adaptive) <= kAdaptTZ;
 }
@@ -918,17 +1009,16 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
   if (n <= 0) return;
   const TrialArgs A = trial_args(x, n, P, K, out, zeros, evals, status, logp);
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  const int depth = tree_depth(P, K);
   if (evals) {
-    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, depth, s, fast_done);
+    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, s, fast_done);
     else if (out_kind == OUT_ARRAY)
-      launch_mode<true, OUT_ARRAY>(mode, part, A, W, depth, s, fast_done);
-    else launch_mode<true, OUT_LOGP>(mode, part, A, W, depth, s, fast_done);
+      launch_mode<true, OUT_ARRAY>(mode, part, A, W, s, fast_done);
+    else launch_mode<true, OUT_LOGP>(mode, part, A, W, s, fast_done);
   } else {
-    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, depth, s, fast_done);
+    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, s, fast_done);
     else if (out_kind == OUT_ARRAY)
-      launch_mode<false, OUT_ARRAY>(mode, part, A, W, depth, s, fast_done);
-    else launch_mode<false, OUT_LOGP>(mode, part, A, W, depth, s, fast_done);
+      launch_mode<false, OUT_ARRAY>(mode, part, A, W, s, fast_done);
+    else launch_mode<false, OUT_LOGP>(mode, part, A, W, s, fast_done);
   }
 }
 

@@ -152,6 +152,14 @@ int wfpt_profile_enable(wfpt_ctx *ctx, int flags);
  * the last reset. */
 int wfpt_profile_read(wfpt_ctx *ctx, double *kernel_ms, int64_t *launches, int64_t *n_evals,
                       int reset);
+/* Refinement work of the adaptive calls made under WFPT_PROF_EVALS since the
+ * last reset (synchronises the stream): counts[L] (L = 1, 2) t-node (or z
+ * grid) evaluations of tree level L, counts[4] trials whose root interval was
+ * refined, counts[5] trials settled on the exact path, counts[6] trials
+ * continued on the per-lane walk, counts[7] z walks (counts[8 + L]: at tree
+ * level L). counts[11..15]: per-phase engine time of diagnostic builds
+ * (WFPT_PHASE_TIMING), kilo-cycles summed over waves. */
+int wfpt_profile_lists(wfpt_ctx *ctx, int64_t counts[16], int reset);
 int wfpt_synchronize(wfpt_ctx *ctx);
 
 #ifdef __cplusplus

@@ -49,6 +49,7 @@ def main():
         ctx.profile(ctx.PROF_EVALS)
         ds.wiener_like(*p, *KN)
         _, _, ne = ctx.profile_read(reset=True)
+        lists = ctx.profile_lists(reset=True)
         ctx.profile(0)
         for _ in range(3):
             ds.wiener_like(*p, *KN)
@@ -64,9 +65,14 @@ def main():
             ds.wiener_like(*p, *KN)
         k_ms, nl, _ = ctx.profile_read(reset=True)
         ctx.profile(0)
+        ctx.profile_lists(reset=True)
+        for _ in range(a.reps):
+            ds.wiener_like(*p, *KN)
+        ph = ctx.profile_lists(reset=True).get("phase_kcycles", [])
+        lists["phase_kcycles_per_call"] = [round(v / a.reps) for v in ph]
         rows.append({"params": [round(float(v), 4) for v in p], "trials": x.size,
                      "evals_per_trial": ne / x.size, "call_ms": el * 1e3,
-                     "fast_kernel_ms": k_ms / max(nl, 1)})
+                     "fast_kernel_ms": k_ms / max(nl, 1), "lists": lists})
         print(json.dumps(rows[-1]), flush=True)
         del ds
     st = rows[:4]
