@@ -85,8 +85,9 @@ wfpt_profile_read = _sig("wfpt_profile_read", _I,
                          [_VP, _PD, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I])
 try:  # diagnostics only: A/B runs may load an older library build without it
     wfpt_profile_lists = _sig("wfpt_profile_lists", _I, [_VP, ctypes.POINTER(_I64), _I])
+    wfpt_debug_waves = _sig("wfpt_debug_waves", _I, [_VP, ctypes.POINTER(ctypes.c_uint64), _I64])
 except AttributeError:
-    wfpt_profile_lists = None
+    wfpt_profile_lists = wfpt_debug_waves = None
 wfpt_synchronize = _sig("wfpt_synchronize", _I, [_VP])
 wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
@@ -96,7 +97,7 @@ EXPORTED = [
     "wfpt_wiener_like_host", "wfpt_wiener_like_nodes", "wfpt_pdf_array", "wfpt_full_pdf",
     "wfpt_wiener_like_multi", "wfpt_dmat_cdf_array", "wfpt_comm_unique_id", "wfpt_comm_init",
     "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
-    "wfpt_decode_result", "wfpt_profile_lists",
+    "wfpt_decode_result", "wfpt_profile_lists", "wfpt_debug_waves",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)
@@ -169,6 +170,12 @@ class Context:
         return {"tasks1": v[1], "tasks2": v[2], "records": v[4], "exact": v[5],
                 "walk": v[6], "zwalks": v[7], "zwalks0": v[8], "zwalks1": v[9],
                 "zwalks2": v[10], "phase_kcycles": v[11:16]}
+
+    def debug_waves(self, n):
+        """Per-wave engine records of diagnostic builds (wfpt_debug_waves): (n, 8) uint64."""
+        out = np.zeros((n, 8), dtype=np.uint64)
+        check(wfpt_debug_waves(self.handle, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), n))
+        return out
 
     def synchronize(self):
         check(wfpt_synchronize(self.handle))

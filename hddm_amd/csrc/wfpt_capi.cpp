@@ -109,7 +109,8 @@ struct wfpt_ctx {
   DevBuf<unsigned char> wl;  // lane of the deferred trial in each slot
   DevBuf<int> wl_n;          // per chunk: deferred trials
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
-  int* prof = nullptr;       // device: 16 deferred-pass work counters (PROF_EVALS)
+  int* prof = nullptr;       // device: 16 refinement work counters (PROF_EVALS)
+  unsigned long long* phase = nullptr;  // device: engine phase cycles (diagnostic builds)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
@@ -117,7 +118,7 @@ struct wfpt_ctx {
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
-  double* mres = nullptr;      // mapped pinned {sum, zeros, errors, deferred, word}
+  double* mres = nullptr;      // mapped pinned {sum, zeros, errors, deferred, word, heavy}
   double* mres_dev = nullptr;  // its device alias
   unsigned long long seq = 0;  // completion word finalize writes to mres[4]
   MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
@@ -135,6 +136,8 @@ struct wfpt_ctx {
   int nranks = 1, rank = 0;
 };
 
+constexpr int64_t kSplitCap = 8192;  // heavy chunks a dataset records per call
+
 struct wfpt_ds {
   wfpt_ctx* ctx = nullptr;
   int64_t n = 0;
@@ -145,6 +148,19 @@ struct wfpt_ds {
   // the last call on this dataset deferred no trial: the next one runs the
   // level-0 pass + finalize only (run_sum_fast), no slow pass
   mutable bool no_defer = false;
+  // heavy-chunk record (wfpt_internal.h: Split), double-buffered by call
+  // parity: the engine writes [1 - parity] while it reads [parity]
+  int64_t nw = 0;
+  int split_cap = 0;
+  unsigned char* hpred[2] = {nullptr, nullptr};
+  int* hlist[2] = {nullptr, nullptr};
+  int* hcount = nullptr;  // [2]
+  double* hlp = nullptr;
+  int* hmeta = nullptr;
+  int* hdone = nullptr;
+  int* hzn = nullptr;
+  mutable int nsplit = 0;  // chunks the next call splits
+  mutable int parity = 0;
 };
 
 namespace {
@@ -219,6 +235,7 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   W->wl_n = c->wl_n.p;
   W->rflag = c->rflag.p;
   W->prof = c->prof;
+  W->phase = c->phase;
   W->nslots = ns;
   return WFPT_OK;
 }
@@ -241,12 +258,50 @@ int check_status_value(double enc) {
   return fail(WFPT_ERR_UNSUPPORTED, msg);
 }
 
+// The dataset's heavy-chunk state for one engine call (null: no split, no
+// record).
+wfpt::Split split_of(const wfpt_ds* d) {
+  wfpt::Split S{};
+  if (!d || !d->hcount) return S;
+  const int cur = d->parity, nx = 1 - cur;
+  S.n = d->nsplit;
+  S.cap = d->split_cap;
+  S.list = d->hlist[cur];
+  S.pred = d->hpred[cur];
+  S.next_pred = d->hpred[nx];
+  S.next_list = d->hlist[nx];
+  S.next_n = d->hcount + nx;
+  S.lp = d->hlp;
+  S.meta = d->hmeta;
+  S.done = d->hdone;
+  S.zn = d->hzn;
+  return S;
+}
+
+// After a call's result r is in host memory: the next call splits the heavy
+// chunks this one recorded (engine calls), or none.
+void split_advance(const wfpt_ds* d, bool engine, const double* r) {
+  if (!d) return;
+  if (!engine || !d->hcount) {
+    d->nsplit = 0;
+    return;
+  }
+  d->nsplit = (int)std::min<double>(r[5], (double)d->split_cap);
+  d->parity = 1 - d->parity;
+}
+
+bool engine_family(const wfpt::Params& P, const wfpt::Knobs& K) {
+  const int m = wfpt::select_mode(P.sz, P.st, K.use_adaptive);
+  return m >= wfpt::kAdaptT && m <= wfpt::kAdaptTZ;
+}
+
 // Likelihood sum over device x[n]: adaptive / direct families run the level-0
 // pass and (part & kPassDeferred) the deferred-trial pass, fixed Simpson one
 // trial kernel; then finalize writes {sum, zeros, errors, deferred} + the
 // completion word to `out` (mapped host memory or device).
 int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
-            const wfpt::Knobs& K, double* out, int part = wfpt::kPassAll) {
+            const wfpt::Knobs& K, double* out, int part = wfpt::kPassAll,
+            const wfpt_ds* d = nullptr) {
   const int64_t nb = wfpt::partials_for(n, P, K);
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
@@ -259,13 +314,16 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   // the one rocprofv3 reports as fast_kernel<...>)
   const bool prof = c->profile && (part & wfpt::kPassFast);
   if (prof) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  const bool eng = d && d->hcount && engine_family(P, K);
+  const wfpt::Split S = eng ? split_of(d) : wfpt::Split{};
   wfpt::launch_trials(0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p, c->zero.p,
                       c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
-                      prof ? c->ev1 : nullptr);
+                      prof ? c->ev1 : nullptr, &S);
   HIP_TRY(hipGetLastError());
   const int64_t nw = (n + 63) / 64;
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? W.wl_n : nullptr, adaptive ? nw : 0,
-                        c->status, out, ++c->seq, c->stream);
+                        c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
+                        eng ? d->hcount + d->parity : nullptr);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -346,13 +404,19 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
                  double* out) {
   const int64_t n = d->n;
   if (c->count || !d->no_defer || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
-  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassFast)) return rc;
+  const bool eng = engine_family(P, K);
+  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassFast, d)) return rc;
   if (int rc = wait_result(c, c->mres)) return rc;
-  if (c->mres[3] == 0.0) return decode_sum(c, c->mres, out);
+  if (c->mres[3] == 0.0) {
+    split_advance(d, eng, c->mres);
+    return decode_sum(c, c->mres, out);
+  }
   d->no_defer = false;
   if (int rc = check_status_value(c->mres[2])) return rc;
-  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassDeferred)) return rc;
-  return read_sum(c, c->mres, out);
+  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassDeferred, d)) return rc;
+  if (int rc = wait_result(c, c->mres)) return rc;
+  split_advance(d, eng, c->mres);
+  return decode_sum(c, c->mres, out);
 }
 
 int upload(wfpt_ctx* c, const double* x, int64_t n) {
@@ -403,14 +467,18 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->host_status, sizeof(int), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemset(c->status, 0, sizeof(int));
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&c->mres, 5 * sizeof(double),
+    e = hipHostMalloc((void**)&c->mres, 6 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->prof, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->prof, 0, 16 * sizeof(int));
-  if (e == hipSuccess) std::memset(c->mres, 0, 5 * sizeof(double));
+  if (e == hipSuccess)
+    e = hipMalloc((void**)&c->phase, 8 * wfpt::kPhaseWaves * sizeof(unsigned long long));
+  if (e == hipSuccess)
+    e = hipMemset(c->phase, 0, 8 * wfpt::kPhaseWaves * sizeof(unsigned long long));
+  if (e == hipSuccess) std::memset(c->mres, 0, 6 * sizeof(double));
   if (e != hipSuccess) {
     wfpt_close(c);
     return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
@@ -436,6 +504,7 @@ void wfpt_close(wfpt_ctx* c) {
   c->wl_n.release();
   c->rflag.release();
   if (c->prof) (void)hipFree(c->prof);
+  if (c->phase) (void)hipFree(c->phase);
   c->defer.release();
   c->nd_idx.release();
   c->nd_par.release();
@@ -513,6 +582,23 @@ int wfpt_dataset_create(wfpt_ctx* c, const double* rt, int64_t n, const int32_t*
     if (e == hipSuccess)
       e = hipMemcpy(d->off, off.data(), (n_nodes + 1) * sizeof(int64_t), hipMemcpyHostToDevice);
   }
+  // heavy-chunk record (Split): lists sized for up to kSplitCap chunks
+  d->nw = (n + 63) / 64;
+  d->split_cap = (int)std::min<int64_t>(std::max<int64_t>(d->nw, 1), kSplitCap);
+  const int64_t nwb = std::max<int64_t>(d->nw, 1);
+  for (int k = 0; k < 2 && e == hipSuccess; ++k) {
+    e = hipMalloc((void**)&d->hpred[k], nwb);
+    if (e == hipSuccess) e = hipMemset(d->hpred[k], 0, nwb);
+    if (e == hipSuccess) e = hipMalloc((void**)&d->hlist[k], d->split_cap * sizeof(int));
+  }
+  if (e == hipSuccess) e = hipMalloc((void**)&d->hcount, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(d->hcount, 0, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&d->hlp, (size_t)d->split_cap * 64 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&d->hmeta, (size_t)d->split_cap * 64 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&d->hdone, d->split_cap * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(d->hdone, 0, d->split_cap * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&d->hzn, d->split_cap * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(d->hzn, 0, d->split_cap * sizeof(int));
   if (e != hipSuccess) {
     wfpt_dataset_destroy(d);
     return fail(WFPT_ERR_HIP, std::string("wfpt_dataset_create: ") + hipGetErrorString(e));
@@ -527,6 +613,15 @@ void wfpt_dataset_destroy(wfpt_ds* d) {
   if (d->x) (void)hipFree(d->x);
   if (d->node) (void)hipFree(d->node);
   if (d->off) (void)hipFree(d->off);
+  for (int k = 0; k < 2; ++k) {
+    if (d->hpred[k]) (void)hipFree(d->hpred[k]);
+    if (d->hlist[k]) (void)hipFree(d->hlist[k]);
+  }
+  if (d->hcount) (void)hipFree(d->hcount);
+  if (d->hlp) (void)hipFree(d->hlp);
+  if (d->hmeta) (void)hipFree(d->hmeta);
+  if (d->hdone) (void)hipFree(d->hdone);
+  if (d->hzn) (void)hipFree(d->hzn);
   delete d;
 }
 
@@ -546,9 +641,11 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
   DeviceGuard g(c->device);
   int rc = run_sum_fast(c, d, P, K, out);
   if (rc >= 0) return rc;
-  if (int rc2 = run_sum(c, d->x, d->n, P, K, c->mres_dev)) return rc2;
+  if (int rc2 = run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassAll, d)) return rc2;
   bool deferred = true;
-  rc = read_sum(c, c->mres, out, &deferred);
+  if (int rc2 = wait_result(c, c->mres)) return rc2;
+  split_advance(d, engine_family(P, K), c->mres);
+  rc = decode_sum(c, c->mres, out, &deferred);
   if (rc == WFPT_OK && c->fast_only) d->no_defer = !deferred;
   return rc;
 }
@@ -775,8 +872,8 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  HIP_TRY(c->res.reserve(5));
-  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p)) return rc;
+  HIP_TRY(c->res.reserve(6));
+  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p, wfpt::kPassAll, d)) return rc;
   // {sum, zeros, encoded errors} of every rank summed: any zero trial or
   // failure anywhere reaches every rank (the error encoding keeps depth and
   // budget failures apart under the sum, wfpt_internal.h: kBudgetUnit)
@@ -785,7 +882,9 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   // (run_sum's finalize used the previous one for the device copy)
   wfpt::launch_publish(c->res.p, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
-  return read_sum(c, c->mres, out);
+  if (int rc = wait_result(c, c->mres)) return rc;
+  split_advance(d, engine_family(P, K), c->mres);
+  return decode_sum(c, c->mres, out);
 }
 
 int wfpt_profile_enable(wfpt_ctx* c, int flags) {
@@ -819,7 +918,27 @@ int wfpt_profile_lists(wfpt_ctx* c, int64_t counts[16], int reset) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipMemcpy(h, c->prof, sizeof(h), hipMemcpyDeviceToHost));
   for (int k = 0; k < 16; ++k) counts[k] = h[k];
-  if (reset) HIP_TRY(hipMemset(c->prof, 0, sizeof(h)));
+  std::vector<unsigned long long> ph(8 * wfpt::kPhaseWaves);
+  HIP_TRY(hipMemcpy(ph.data(), c->phase, ph.size() * sizeof(ph[0]), hipMemcpyDeviceToHost));
+  for (int k = 0; k < 5; ++k) {
+    unsigned long long t = 0;
+    for (int w = 0; w < wfpt::kPhaseWaves; ++w) t += ph[w * 8 + 2 + k];
+    counts[11 + k] = (int64_t)(t / 1000);
+  }
+  if (reset) {
+    HIP_TRY(hipMemset(c->prof, 0, sizeof(h)));
+    HIP_TRY(hipMemset(c->phase, 0, ph.size() * sizeof(ph[0])));
+  }
+  return WFPT_OK;
+}
+
+int wfpt_debug_waves(wfpt_ctx* c, uint64_t* out, int64_t max_records) {
+  if (!c || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const int64_t n = std::min<int64_t>(max_records, wfpt::kPhaseWaves);
+  HIP_TRY(hipMemcpy(out, c->phase, n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return WFPT_OK;
 }
 

@@ -104,7 +104,7 @@ constexpr double kDblMin = 2.2250738585072014e-308;
 // relative (checked against 120-bit arithmetic). 30 fp64 ops instead of OCML's
 // general-range sincospi (127). w == 1 is seeded with the reference's own
 // sin(fl(pi)) = 1.2246e-16 so the z = 1 edge keeps its nonzero value.
-__device__ inline void sincospi01(double w, double& s, double& c) {
+__host__ __device__ inline void sincospi01(double w, double& s, double& c) {
   const double t = 2.0 * w;
   const double n = rint(t);
   const double f = t - n;
@@ -345,7 +345,8 @@ __device__ inline double pdf_sv(double xx, double v, double sv, double a, double
 // ---------------------------------------------------------------------------
 // The reference's stop test of adaptiveSimpsonsAux (integrate.pxi:105 / 170):
 // true = refine. Marks kFlagExact when the test is decided inside kTieBand.
-__device__ inline bool simpson_refine(double S, double S2, double err, int bottom, int& flags) {
+__host__ __device__ inline bool simpson_refine(double S, double S2, double err, int bottom,
+                                               int& flags) {
   if (bottom <= 0) return false;
   const double d = fabs(S2 - S), thr = 15 * err;
   if (fabs(d - thr) <= kTieBand * ((fabs(S) + fabs(S2)) + thr)) flags |= kFlagExact;
@@ -960,7 +961,8 @@ enum Outcome : int { kFinal = 0, kTree = 1, kExact = 2 };
 struct Simp {
   double S, Sl, Sr, S2;
 };
-__device__ inline Simp simp5(double h, double fb, double fd, double fm, double fe, double fu) {
+__host__ __device__ inline Simp simp5(double h, double fb, double fd, double fm, double fe,
+                                     double fu) {
   Simp s;
   s.S = (h / 6) * ((fb + (4 * fm)) + fu);
   s.Sl = (h / 12) * ((fb + (4 * fd)) + fm);
@@ -1113,114 +1115,117 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
   return (p > kExactBelow || structural) ? kFinal : kExact;
 }
 
-// Geometry of tree node (L, m) (m's bits = left/right turns from the root),
-// computed as the reference's recursion does: bounds by the midpoint
-// (ub + lb) / 2 of each parent, S = the parent's Sleft / Sright, err halved
-// per level. F(j) returns the stored value at dyadic point j.
-struct TreeNode {
-  double lb, ub, S, err;
-  int pos, W;
+// The engine's level 0 (kAdaptT / kAdaptTZ): the same operations as
+// fast_level0, factored so that any single t node j of a trial's root
+// interval can be evaluated on its own (a split chunk's level-0 task) with
+// exactly the bits the per-lane loop produces. The z grid is the call's table
+// (EngTables), shared by both.
+struct L0Hints {
+  double qn[5];
+  Decision D0, D4;
+  bool ok0, ok4, shared;
 };
-template <class FV>
-__device__ inline TreeNode tree_node(FV&& F, double lb0, double ub0, double err0, int L, int m) {
-  TreeNode n;
-  n.lb = lb0;
-  n.ub = ub0;
-  n.pos = 0;
-  n.W = kTreeW;
-  n.err = err0;
-  n.S = simp5(ub0 - lb0, F(0), 0.0, F(kTreeW / 2), 0.0, F(kTreeW)).S;
-  for (int l = 0; l < L; ++l) {
-    const int W = n.W;
-    const Simp s = simp5(n.ub - n.lb, F(n.pos), F(n.pos + W / 4), F(n.pos + W / 2),
-                         F(n.pos + 3 * W / 4), F(n.pos + W));
-    const double c = (n.ub + n.lb) / 2.;
-    if ((m >> (L - 1 - l)) & 1) {
-      n.lb = c;
-      n.S = s.Sr;
-      n.pos += W / 2;
-    } else {
-      n.ub = c;
-      n.S = s.Sl;
-    }
-    n.W = W / 2;
-    n.err = n.err / 2;
+__device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, double err) {
+  L0Hints H;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) H.qn[j] = -1.0;
+  H.D0 = Decision{0, 0, 0};
+  H.D4 = Decision{0, 0, 0};
+  H.ok0 = H.ok4 = H.shared = false;
+  const double a2 = a * a;
+  const double q0 = exp((-kPi2 * ((x - lb) / a2)) / 2.0);
+  const double R = exp((kPi2 * (ub - lb)) / (8.0 * a2));
+  if (q0 > 1e-280 && R < 1e10 && x - lb > 0) {
+    const double R2 = R * R;
+    H.qn[0] = q0;
+    H.qn[1] = q0 * R;
+    H.qn[2] = q0 * R2;
+    H.qn[3] = q0 * (R2 * R);
+    H.qn[4] = q0 * (R2 * R2);
   }
-  return n;
+  if (x - ub > 0) {
+    float args0, args4;
+    H.ok0 = decide32((x - lb) / a2, err, H.D0, args0);
+    H.ok4 = decide32((x - ub) / a2, err, H.D4, args4);
+    H.shared = H.ok0 && H.ok4 && args0 < 0.5f && H.D0.small == H.D4.small && H.D0.K == H.D4.K;
+  }
+  return H;
+}
+// t node j (0..4: lb, d, c, e, ub) of the trial's root t interval: its value
+// (kAdaptT: pdf_sv / st; kAdaptTZ: the z integral's root estimate / st),
+// kFlagExact in flags for an ambiguous decision or a near-tie, pend = the z
+// integral asks for refinement.
+template <int MODE>
+__device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& K, double lb,
+                                 double ub, const L0Hints& H, int j, const ZGrid& G, int& flags,
+                                 bool& pend, long long& ne) {
+  const double a = P.a, sv = P.sv, err = K.err;
+  const double x = tr.x, v = tr.v, z = tr.z;
+  const double iw = 1.0 / (ub - lb);
+  const double c = (ub + lb) / 2.;
+  const double d = (lb + c) / 2., e = (c + ub) / 2.;
+  const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
+  const double qh =
+      j == 0 ? H.qn[0] : j == 1 ? H.qn[1] : j == 2 ? H.qn[2] : j == 3 ? H.qn[3] : H.qn[4];
+  const bool known = j == 0 ? H.ok0 : (j == 4 ? H.ok4 : H.shared);
+  const TNode T = tnode_setup(x - tc, v, sv, a, err, qh, known, j == 4 ? H.D4 : H.D0);
+  pend = false;
+  if (T.amb) {
+    flags |= kFlagExact;
+    return 0.0;
+  }
+  if (MODE == kAdaptTZ) {
+    const double iZz = 1.0 / ((z + tr.sz / 2.) - (z - tr.sz / 2.));
+    return inner_root(T, G, iZz, v, sv, a, K, flags, ne, pend) * iw;
+  }
+  ne += 1;
+  return tnode_pdf_sv(T, z, v, sv, a) * iw;
 }
 
-// The trial's integral from a completed tree: the reference's recursion
-// (leaf S2 + (S2 - S) / 15, internal left + right) re-walked over the stored
-// values; every stop test repeats the engine's arithmetic, so it takes the
-// same branch. flags gets kFlagExact for a near-tie and kFlagFallback when an
-// interval at depth kTreeDepth still asks for refinement (the tree is deeper
-// than the stored points); nref = refined intervals (each adds 2 nodes x 2
-// evaluations).
-template <class FV>
-__device__ inline double tree_value(FV&& F, double lb0, double ub0, double err0, int depth,
-                                    int& flags, int& nref) {
-  struct Fr {
-    double lb, ub, S, err, left;
-    int pos, W;
-  };
-  Fr stk[kTreeDepth];
-  unsigned right_mask = 0u;
-  int sp = 0, bottom = depth;
-  double lb = lb0, ub = ub0, err = err0;
-  int pos = 0, W = kTreeW;
-  double S = simp5(ub0 - lb0, F(0), 0.0, F(kTreeW / 2), 0.0, F(kTreeW)).S;
-  nref = 0;
-  for (;;) {
-    const Simp s = simp5(ub - lb, F(pos), F(pos + W / 4), F(pos + W / 2), F(pos + 3 * W / 4),
-                         F(pos + W));
-    const bool refine = simpson_refine(S, s.S2, err, bottom, flags);
-    if (refine && sp >= kTreeDepth) flags |= kFlagFallback;
-    if (refine && sp < kTreeDepth) {
-      ++nref;
-      const double c = (ub + lb) / 2.;
+// The engine's level 0 of one trial (as fast_level0, on the table's z grid):
+// kFinal (p), kTree (f[], pend) or kExact.
+template <int MODE>
+__device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
+                                 double& p, double (&f)[5], long long& ne, unsigned& pend) {
+  const Trial tr = trial_setup(x0, P);
+  p = 0.0;
+  pend = 0u;
+  if (!tr.valid) return kFinal;
+  double lb, ub;
+  tree_root<MODE>(tr, P, lb, ub);
+  int flags = 0;
+  if (MODE == kAdaptZ) {
+    const double iw = 1.0 / (ub - lb);
+    const TNode T = tnode_setup(tr.x - P.t, tr.v, P.sv, P.a, K.err);
+    if (T.amb) return kExact;
+    tnode_pdf_sv_grid5(T, G, tr.v, P.sv, P.a, f);
 #pragma unroll
-      for (int k = 0; k < kTreeDepth; ++k)
-        if (k == sp) stk[k] = Fr{c, ub, s.Sr, err / 2, 0.0, pos + W / 2, W / 2};
-      ++sp;
-      ub = c;
-      S = s.Sl;
-      err = err / 2;
-      W = W / 2;
-      bottom -= 1;
-      continue;
+    for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
+    ne += 5;
+  } else {
+    const L0Hints H = l0_hints(tr.x, lb, ub, P.a, K.err);
+#pragma unroll 1
+    for (int j = 0; j < 5; ++j) {
+      bool pj;
+      const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne);
+      if (flags & kFlagExact) return kExact;
+      if (pj) pend |= 1u << (j * (kTreeW / 4));
+      if (j == 0) f[0] = y;
+      else if (j == 1) f[1] = y;
+      else if (j == 2) f[2] = y;
+      else if (j == 3) f[3] = y;
+      else f[4] = y;
     }
-    double val = s.S2 + (s.S2 - S) / 15;
-    bool done = false;
-    for (;;) {
-      if (sp == 0) {
-        done = true;
-        break;
-      }
-      const int top = sp - 1;
-      Fr fr = stk[0];
-#pragma unroll
-      for (int k = 1; k < kTreeDepth; ++k)
-        if (k == top) fr = stk[k];
-      if (!((right_mask >> top) & 1u)) {
-#pragma unroll
-        for (int k = 0; k < kTreeDepth; ++k)
-          if (k == top) stk[k].left = val;
-        right_mask |= 1u << top;
-        lb = fr.lb;
-        ub = fr.ub;
-        S = fr.S;
-        err = fr.err;
-        pos = fr.pos;
-        W = fr.W;
-        bottom = depth - sp;
-        break;
-      }
-      val = fr.left + val;
-      right_mask &= ~(1u << top);
-      --sp;
-    }
-    if (done) return val;
   }
+  if (pend) return kTree;
+  const Simp s = simp5(ub - lb, f[0], f[1], f[2], f[3], f[4]);
+  const int bottom = (MODE == kAdaptZ) ? K.n_sz : K.n_st;
+  const bool refine = simpson_refine(s.S, s.S2, K.simps_err, bottom, flags);
+  if (flags & kFlagExact) return kExact;
+  if (refine) return kTree;
+  p = s.S2 + (s.S2 - s.S) / 15;
+  const bool structural = (MODE == kAdaptZ) ? tr.x - P.t <= 0 : tr.x - lb <= 0;
+  return (p > kExactBelow || structural) ? kFinal : kExact;
 }
 
 // z grids of the engine, relative to the dyadic points P of [lb_z, ub_z]:
@@ -1253,7 +1258,8 @@ __host__ __device__ inline double dyadic_point(double lb, double ub, int k) {
   }
 }
 
-__device__ inline ZGrid zgrid_of(double lb, double ub, int sel, double v, double sv, double a) {
+__host__ __device__ inline ZGrid zgrid_of(double lb, double ub, int sel, double v, double sv,
+                                          double a) {
   ZGrid G;
   const int k0 = sel == kGridRoot ? 0 : sel == kGridL1 ? 2 : sel == kGridL2L ? 1 : 7;
   const int dk = sel == kGridRoot ? 4 : sel == kGridL1 ? 4 : 2;
@@ -1275,6 +1281,83 @@ __device__ inline ZGrid zgrid_of(double lb, double ub, int sel, double v, double
     }
   }
   return G;
+}
+
+
+// The reference's recursion (adaptiveSimpsonsAux, integrate.pxi:94-112 /
+// 159-178) over a tree of depth <= kTreeDepth whose values f[k] at the dyadic
+// points P[k] of the root interval are in registers, in straight-line form:
+// prologue S of the root, then per visited interval its S2 from its 5 values,
+// the stop test (bottom = depth - level, eps halved per level) and either the
+// leaf value S2 + (S2 - S) / 15 or left + right. lv: the deepest level whose
+// values are known. Returns the integral when no visited interval asks for
+// values below lv; otherwise need = the refining intervals of level lv
+// (bit m: interval m of that level), and for lv == kTreeDepth those mean a
+// deeper tree. flags gets kFlagExact for a stop test inside kTieBand; nref =
+// visited refined intervals (2 new nodes x 2 evaluations each).
+__host__ __device__ inline double tree17(const double (&f)[kTreePoints],
+                                         const double (&P)[kTreePoints], double err, int depth,
+                                         int lv, int& flags, unsigned& need, int& nref) {
+  need = 0u;
+  nref = 0;
+  const double h0 = P[kTreeW] - P[0];
+  const double S0 = (h0 / 6) * ((f[0] + (4 * f[8])) + f[16]);
+  const Simp r = simp5(h0, f[0], f[4], f[8], f[12], f[16]);
+  if (!simpson_refine(S0, r.S2, err, depth, flags)) return r.S2 + (r.S2 - S0) / 15;
+  nref = 1;
+  if (lv == 0) {
+    need = 1u;
+    return 0.0;
+  }
+  double vh[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int lo = 8 * m;
+    const double S = m ? r.Sr : r.Sl;
+    const Simp s = simp5(P[lo + 8] - P[lo], f[lo], f[lo + 2], f[lo + 4], f[lo + 6], f[lo + 8]);
+    if (!simpson_refine(S, s.S2, err / 2, depth - 1, flags)) {
+      vh[m] = s.S2 + (s.S2 - S) / 15;
+      continue;
+    }
+    ++nref;
+    if (lv == 1) {
+      need |= 1u << m;
+      vh[m] = 0.0;
+      continue;
+    }
+    double vq[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int l2 = lo + 4 * q;
+      const double Sq = q ? s.Sr : s.Sl;
+      const Simp u = simp5(P[l2 + 4] - P[l2], f[l2], f[l2 + 1], f[l2 + 2], f[l2 + 3], f[l2 + 4]);
+      if (simpson_refine(Sq, u.S2, (err / 2) / 2, depth - 2, flags)) need |= 1u << (2 * m + q);
+      vq[q] = u.S2 + (u.S2 - Sq) / 15;
+    }
+    vh[m] = vq[0] + vq[1];
+  }
+  return need ? 0.0 : vh[0] + vh[1];
+}
+
+// Per-call tables of the engine (host-computed from the call's parameters,
+// passed by value): the z grids of both boundaries (trial_setup's flip x > 0:
+// v = -v, z = 1 - z), the dyadic points of the t tree and of both z trees.
+struct EngTables {
+  ZGrid G[2][4];
+  double tP[kTreePoints];
+  double zP[2][kTreePoints];
+  double iz[2];  // 1 / (ub_z - lb_z) per boundary
+};
+
+__host__ __device__ inline void eng_tables(const Params& P, EngTables& T) {
+  for (int k = 0; k < kTreePoints; ++k) T.tP[k] = dyadic_point(P.t - P.st / 2., P.t + P.st / 2., k);
+  for (int flip = 0; flip < 2; ++flip) {
+    const double zf = flip ? 1. - P.z : P.z, vf = flip ? -P.v : P.v;
+    const double zl = zf - P.sz / 2., zu = zf + P.sz / 2.;
+    for (int sel = 0; sel < 4; ++sel) T.G[flip][sel] = zgrid_of(zl, zu, sel, vf, P.sv, P.a);
+    for (int k = 0; k < kTreePoints; ++k) T.zP[flip][k] = dyadic_point(zl, zu, k);
+    T.iz[flip] = 1.0 / (zu - zl);
+  }
 }
 
 // P(hit upper boundary), pdf.pxi:67-72

@@ -22,8 +22,31 @@ struct Work {
   unsigned char* wl;  // [nslots] lane of the trial in slot
   int* wl_n;          // [chunks] deferred trials of the chunk
   int* rflag;         // [nslots] kFlagExact | kFlagFallback of the trial in slot
-  int* prof;          // [16] deferred-pass work counters (evaluation counting only)
+  int* prof;          // [16] refinement work counters (evaluation counting only)
+  unsigned long long* phase;  // [8 * kPhaseWaves] per-wave engine timing (WFPT_PHASE_TIMING)
   int64_t nslots;
+};
+
+constexpr int kPhaseWaves = 16384;
+
+// Heavy chunks of a resident dataset (wfpt_kernels.hip: engine_kernel). The
+// engine records the chunks whose level 0 leaves more than kHeavyZ z walks
+// (next_*); the following call splits those chunks into kSplit units of
+// kSplitTrials trials, one wave each. All pointers null / n = 0: no split, no
+// record (host arrays, non-engine families).
+constexpr int kSplit = 8, kSplitTrials = 64 / kSplit;
+struct Split {
+  int n;                       // chunks split in this call (their units come first)
+  int cap;                     // capacity of the chunk lists and per-chunk state
+  const int* list;             // [n] their chunk ids
+  const unsigned char* pred;   // [chunks] 1 = split in this call
+  unsigned char* next_pred;    // [chunks] this call's record for the next call
+  int* next_list;              // [cap]
+  int* next_n;                 // device counter (0 at the call's start)
+  double* lp;                  // [cap * 64] per-trial log terms of split chunks
+  int* meta;                   // [cap * 64] zero | defer << 1 | rflag << 2
+  int* done;                   // [cap] units finished (0 at rest)
+  int* zn;                     // [cap] level-0 z walks summed over units (0 at rest)
 };
 
 // Error flags encoded as counts in one double that survives an RCCL sum:
@@ -46,13 +69,17 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3;
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
-                   int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr);
+                   int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,
+                   const Split* split = nullptr);
 // out[0..3] = {sum of nb partials, #zero trials, encoded error flags, deferred
-// (any wl_n[0..nw) != 0; wl_n may be null)}, then out[4] = seq (a 64-bit
-// word) once they are visible; resets *status to 0.
+// (any wl_n[0..nw) != 0; wl_n may be null)}, out[5] = *split_rd (the heavy
+// chunks the call recorded, or 0; then *split_rs = 0), then out[4] = seq (a
+// 64-bit word) once they are visible; resets *status to 0.
 void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
-                     int* status, double* out, unsigned long long seq, hipStream_t s);
-// res[0..2] (device) -> out[0..2] (mapped host), out[3] = 0, then out[4] = seq.
+                     int* status, double* out, unsigned long long seq, hipStream_t s,
+                     const int* split_rd = nullptr, int* split_rs = nullptr);
+// res[0..2], res[5] (device) -> out[0..2], out[5] (mapped host), out[3] = 0,
+// then out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
 // two-pass fast path; d_idx / d_par hold up to n deferred trials, *n_defer

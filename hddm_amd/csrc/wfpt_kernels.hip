@@ -173,45 +173,59 @@ void fast_kernel(TrialArgs A, Work W) {
 // The engine of the adaptive families (kAdaptT, kAdaptZ, kAdaptTZ;
 // integrate.pxi:72-206 driven by pdf.pxi:132-146). One wave owns a chunk of 64
 // consecutive trials and completes their quadrature trees, up to kTreeDepth
-// refinement levels per axis (HDDM's n_st = n_sz = 2), without leaving the
-// wave:
-//   * a task is one evaluation of a trial's integrand at one t node: a 5-wide
-//     z grid (kAdaptZ, kAdaptTZ: tnode_pdf_sv_grid5) or one pdf_sv (kAdaptT).
-//     Level 0 is each lane's own root interval (its 5 t nodes, or its root z
-//     grid). The stop tests of level L (each lane its own tree, in the
-//     reference's order and arithmetic) queue level L + 1's tasks in LDS;
-//     rounds of 64 tasks spread them over the wave's lanes, so the cost of a
-//     level is ceil(tasks / 64) rounds and a chunk with few refining trials
-//     pays few rounds;
+// refinement levels per axis (HDDM's n_st = n_sz = 2):
+//   * level 0 runs in registers, each lane its own trial (fast_level0: its
+//     root interval's 5 t nodes with shared series decisions and the q
+//     recurrence, or its root z grid); a chunk none of whose trials refines
+//     ends there;
+//   * refinement runs in rounds (refine_rounds). A task is one evaluation of a
+//     trial's integrand at one t node: a 5-wide z grid (kAdaptZ, kAdaptTZ:
+//     tnode_pdf_sv_grid5) or one pdf_sv (kAdaptT). The stop tests of level L
+//     (each lane its own tree: tree17, the reference's recursion in
+//     straight-line form over the values in registers) queue level L + 1's
+//     tasks in LDS, and each round gives every lane of the team one task;
 //   * kAdaptTZ: a t node whose z integral asks for refinement queues a z walk:
 //     4 lanes evaluate its 4 z grids (the root again, L1, L2L, L2R: every z
-//     node a depth-2 walk can reach, 16 walks per round), then one lane walks
-//     the z tree over those 17 values (tree_value), in the reference's order;
-//   * every evaluation goes through one code site (the loop of rounds), so the
-//     series code is instantiated once.
-// Data in LDS per wave: the trees' values F[point * 64 + owner lane], the z
-// walks' values, the task queues, the owners' x and flags; per block: the z
-// grids of both boundaries and the t tree's dyadic points.
+//     node a depth-2 walk can reach), then one lane runs tree17 over the z
+//     tree's 17 values;
+//   * every evaluation of the rounds goes through one code site.
+// Heavy chunks: a chunk whose level 0 leaves more than kHeavyZ z walks (the
+// shortest RTs, where every t node's z integral refines) would serialise
+// tens of rounds in one wave and set the launch's length. On a resident
+// dataset the engine records such chunks (Split, next_*); the following call
+// runs each of them as kSplit units of kSplitTrials trials, one wave each,
+// dispatched first: the unit's level 0 runs as tasks (l0_node, bit-identical
+// to the per-lane loop) and its refinement spreads over the whole wave. The
+// last unit of a chunk to finish folds the chunk's per-trial terms in the
+// same order wave_sum uses, so a chunk's partial does not depend on whether
+// it was split (likelihoods stay bitwise reproducible across call histories).
 // Trials whose value hinges on last-bit rounding (kFlagExact) or whose tree is
 // deeper (kFlagFallback) become deferred slots for fold_kernel.
-constexpr int kEngBlock = 256;
+#ifndef WFPT_ENG_BLOCK
+#define WFPT_ENG_BLOCK 256
+#endif
+#ifndef WFPT_HEAVY_Z
+#define WFPT_HEAVY_Z 96
+#endif
+constexpr int kEngBlock = WFPT_ENG_BLOCK;
 constexpr int kEngWaves = kEngBlock / 64;
-constexpr int kZBatch = 16;                             // z walks per round
-constexpr int kQCap = 2 * (1 << kTreeDepth) * 64;      // tasks of one level
-constexpr int kFlagIdle = 16;                           // lane without a trial to integrate
+constexpr int kHeavyZ = WFPT_HEAVY_Z;
+constexpr int kQCap = 2 * (1 << kTreeDepth) * 64;  // tasks (or z walks) of one level
+constexpr int kFlagIdle = 16;                       // lane without a trial to integrate
 constexpr int kFlagStop = kFlagExact | kFlagFallback | kFlagIdle;
 
-struct EngWave {
-  double F[kTreePoints * 64];       // tree values: point * 64 + owner
-  double ZV[kZBatch * kTreePoints];  // the current round's z walks
-  double X[64];                      // the owners' x
-  ZGrid G[2][4];                     // [x > 0][GridSel]: z grids of each boundary's root z interval
-  double tc[kTreePoints];            // the t tree's dyadic points
-  double lbz[2], ubz[2], hz[2], iz[2];  // per boundary: z interval, width, 1 / width
-  int fl[64];                        // the owners' flags
-  int cnt[64];                       // the owners' pdf_sv evaluations (COUNT)
-  uint16_t Q[kQCap];                 // tasks of the current level: owner | point << 6 | grid << 11
-  uint16_t ZQ[kQCap];                // z walks of the current level: owner | point << 6
+// LDS of one chunk under refinement by a team of TW waves.
+template <int TW>
+struct ChunkLds {
+  double F[kTreePoints * 64];              // tree values: point * 64 + owner lane
+  double ZV[16 * TW * kTreePoints];        // the current round's z walks
+  double X[64];                            // the owners' x
+  EngTables tab;                           // the call's tables
+  int fl[64];                              // the owners' flags
+  int cnt[64];                             // the owners' pdf_sv evaluations (COUNT)
+  int qn[2];                               // lengths of Q and ZQ
+  uint16_t Q[kQCap];                       // tasks of the level: owner | point << 6 | grid << 11
+  uint16_t ZQ[kQCap];                      // z walks of the level: owner | point << 6
 };
 
 __device__ inline void wave_sync() {
@@ -219,14 +233,22 @@ __device__ inline void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+template <int TW>
+__device__ inline void team_sync() {
+  if (TW == 1) wave_sync();
+  else __syncthreads();
+}
 
-// Appends `code` of every flagged lane to q[base...] in lane order; returns
-// the new length (wave-uniform).
-__device__ inline int wave_append(bool flag, int code, uint16_t* q, int base) {
+// Appends `code` of every flagged lane of this wave to q at the LDS length
+// counter *n (one LDS atomic per wave). Read *n after the next team_sync.
+__device__ inline void team_push(bool flag, int code, uint16_t* q, int* n) {
   const int lane = threadIdx.x & 63;
   const unsigned long long b = __ballot(flag);
+  if (!b) return;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(n, __popcll(b));
+  base = __shfl(base, 0, 64);
   if (flag) q[base + __popcll(b & lanemask_lt(lane))] = (uint16_t)code;
-  return base + __popcll(b);
 }
 
 // Point of value y[j] of a grid (GridSel) and whether this grid supplies it.
@@ -238,271 +260,267 @@ __device__ inline bool grid_owns(int gs, int j) {
   return gs == kGridRoot ? true : gs == kGridL2R ? j > 0 : j < 4;
 }
 
+template <int TW>
+__device__ inline void load_tables(ChunkLds<TW>& cl, const EngTables& tab, int tid) {
+  const double* src = reinterpret_cast<const double*>(&tab);
+  double* dst = reinterpret_cast<double*>(&cl.tab);
+  for (int k = tid; k < (int)(sizeof(EngTables) / sizeof(double)); k += 64 * TW) dst[k] = src[k];
+}
+
+// Own tree of owner lane `o` in registers.
+template <int TW>
+__device__ inline void load_tree(const ChunkLds<TW>& cl, int o, double (&f)[kTreePoints]) {
+#pragma unroll
+  for (int k = 0; k < kTreePoints; ++k) f[k] = cl.F[k * 64 + o];
+}
+
+// Work tallies of one chunk (COUNT builds; wfpt_profile_lists).
+struct Tally {
+  int t1 = 0, t2 = 0, rec = 0, z[3] = {0, 0, 0};
+};
+
 // WFPT_PHASE_TIMING (diagnostic builds): shader-clock time per engine phase,
-// summed over waves into W.prof[11..15] in units of 1024 cycles (level 0,
-// tables, z rounds, t rounds, tests + epilogue).
+// per wave in W.phase (level 0, tables, z rounds, t rounds, tests + epilogue;
+// wfpt_profile_lists reports the sums in kilo-cycles, wfpt_debug_waves the
+// per-wave records).
 #ifdef WFPT_PHASE_TIMING
-#define PHASE_MARK(k)                                    \
-  do {                                                   \
-    const long long now_ = __builtin_amdgcn_s_memtime(); \
-    ph[k] += now_ - ph_t;                                \
-    ph_t = now_;                                         \
-  } while (0)
+struct PhaseClock {
+  long long ph[5] = {0, 0, 0, 0, 0};
+  long long t = 0;
+  int nz = 0, nt = 0;
+  __device__ void start() { t = __builtin_amdgcn_s_memtime(); }
+  __device__ void mark(int k) {
+    const long long now = __builtin_amdgcn_s_memtime();
+    ph[k] += now - t;
+    t = now;
+  }
+};
 #else
-#define PHASE_MARK(k) \
-  do {                \
-  } while (0)
+struct PhaseClock {
+  int nz = 0, nt = 0;
+  __device__ void start() {}
+  __device__ void mark(int) {}
+};
 #endif
 
-template <int MODE, bool COUNT, int OUT>
-__global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work W) {
-#ifdef WFPT_PHASE_TIMING
-  long long ph[5] = {0, 0, 0, 0, 0};
-  long long ph_t = __builtin_amdgcn_s_memtime();
-#endif
-  __shared__ EngWave wave_lds[kEngWaves];
-  const int lane = threadIdx.x & 63;
-  EngWave& wv = wave_lds[threadIdx.x >> 6];
-  EngWave& sh = wv;  // per-wave tables: no block barrier anywhere
+// Refinement rounds of one chunk by a team of TW waves (tid = 0..64 TW - 1;
+// the chunk's owner lanes are tid < 64). Entry: stage 1 after level 0 with
+// its values in F and its z walks queued (engine_kernel), or stage 0 with
+// level 0's t nodes (root z grids) queued as tasks (split_unit: they take the
+// level-0 hints, l0_hints, so their bits equal fast per-lane level 0's). All
+// control is team-uniform.
+template <int MODE, bool COUNT, int TW>
+__device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int tid, int stage,
+                                     Tally& ty, PhaseClock& pc) {
+  constexpr int NT = 64 * TW;
   const double v = A.P.v, sv = A.P.sv, a = A.P.a, z = A.P.z, t = A.P.t;
   const double err = A.K.err, se = A.K.simps_err;
   const int nsz = A.K.n_sz;
   const int depth = (MODE == kAdaptZ) ? A.K.n_sz : A.K.n_st;
-  const int64_t i = (int64_t)blockIdx.x * kEngBlock + threadIdx.x;
-  const int64_t c = i >> 6;
-  // (little state lives across level 0: the trial's setup is redone after it)
-  const double* xp = A.x + (i < A.n ? i : 0);
-  // ---- level 0, each lane its own trial, in registers (fast_level0: the
-  // root interval's 5 t nodes with shared series decisions and the q
-  // recurrence, or the root z grid) ----
-  double p = 0.0, f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  long long ne0 = 0;
-  int fl0 = 0, oc = kFinal;
-  unsigned pend0 = 0u;
-  if (i < A.n) oc = fast_level0<MODE>(*xp, A.P, A.K, p, f0, ne0, fl0, pend0);
-  PHASE_MARK(0);
-  const double x0 = i < A.n ? *xp : 0.0;
-  const Trial tr = trial_setup(x0, A.P);
-  double lb, ub;
-  tree_root<MODE>(tr, A.P, lb, ub);
-  const double iw = (MODE == kAdaptZ) ? 0.0 : 1.0 / (ub - lb);
-  wv.X[lane] = x0;
-  wv.fl[lane] = oc == kTree ? 0 : (oc == kExact ? (int)kFlagExact : (int)kFlagIdle);
-  if (COUNT) wv.cnt[lane] = (int)ne0;
-
-  int L = 0, stage = 1, r = 0, nq = 0, nz = 0;
-  unsigned act = 1u;  // own tree: the intervals of level L under test
-  int pq1 = 0, pq2 = 0, prec = 0, pz0 = 0, pz1 = 0, pz2 = 0;  // COUNT: work tallies
-  if (__ballot(oc == kTree)) {
-    // the wave's tables (trial_setup's flip: x > 0 => v = -v, z = 1 - z):
-    // lanes 0..7 one z grid each, lanes 8..24 one t point each
-    if (MODE != kAdaptT && lane < 8) {
-      const int flip = lane >> 2, sel = lane & 3;
-      const double zf = flip ? 1. - z : z, vf = flip ? -v : v;
-      const double zl = zf - A.P.sz / 2., zu = zf + A.P.sz / 2.;
-      sh.G[flip][sel] = zgrid_of(zl, zu, sel, vf, sv, a);
-      if (sel == 0) {
-        sh.lbz[flip] = zl;
-        sh.ubz[flip] = zu;
-        sh.hz[flip] = zu - zl;
-        sh.iz[flip] = 1.0 / (zu - zl);
-      }
-    }
-    if (MODE != kAdaptZ && lane >= 8 && lane < 8 + kTreePoints)
-      sh.tc[lane - 8] = dyadic_point(t - A.P.st / 2., t + A.P.st / 2., lane - 8);
-    // the refining trials' root values (a pending z integral's value comes
-    // from its z walk) and their pending z integrals (kAdaptTZ)
-    if (oc == kTree) {
-#pragma unroll
-      for (int j = 0; j < 5; ++j) wv.F[j * (kTreeW / 4) * 64 + lane] = f0[j];
-    }
-    if (MODE == kAdaptTZ) {
-#pragma unroll
-      for (int j = 0; j < 5; ++j)
-        nz = wave_append(oc == kTree && ((pend0 >> (j * (kTreeW / 4))) & 1u),
-                         lane | ((j * (kTreeW / 4)) << 6), wv.ZQ, nz);
-    }
-    wave_sync();
-    PHASE_MARK(1);
+  const double iwt = 1.0 / (cl.tab.tP[kTreeW] - cl.tab.tP[0]);
+  int L = 0, r = 0;
 #pragma unroll 1
-    for (;;) {
-      if (stage == 0 && r * 64 >= nq) {
-        stage = 1;
-        r = 0;
+  for (;;) {
+    const int nq = cl.qn[0], nz = cl.qn[1];
+    if (stage == 0 && r * NT >= nq) {
+      stage = 1;
+      r = 0;
+    }
+    if (stage == 1 && (MODE != kAdaptTZ || r * 16 * TW >= nz)) stage = 2;
+    if (stage == 2) {
+      pc.mark(2);
+      if (L <= 2) ty.z[L] = nz;
+      // stop tests of level L, each owner lane its own tree
+      unsigned need = 0u;
+      if (tid < 64 && !(cl.fl[tid] & kFlagStop)) {
+        double f[kTreePoints];
+        load_tree(cl, tid, f);
+        const double(&P)[kTreePoints] =
+            (MODE == kAdaptZ) ? cl.tab.zP[cl.X[tid] > 0] : cl.tab.tP;
+        int fl = 0, nref = 0;
+        (void)tree17(f, P, se, depth, L, fl, need, nref);
+        if (L == kTreeDepth && need) fl |= kFlagFallback;  // deeper than the in-wave levels
+        if (fl & (kFlagExact | kFlagFallback)) {
+          atomicOr(&cl.fl[tid], fl & (kFlagExact | kFlagFallback));
+          need = 0u;
+        }
       }
-      if (stage == 1 && (MODE != kAdaptTZ || r * kZBatch >= nz)) stage = 2;
-      if (stage == 2) {
-        PHASE_MARK(2);  // (the t rounds are marked at their end)
-        if (COUNT) {
-          if (L == 0) pz0 = nz;
-          else if (L == 1) pz1 = nz;
-          else pz2 = nz;
-        }
-        // stop tests of level L, each lane its own tree (adaptiveSimpsonsAux,
-        // integrate.pxi:105 / 170): refined intervals make their children
-        // level L + 1's intervals
-        unsigned nxt = 0u;
-        if (!(wv.fl[lane] & kFlagStop)) {
-          int f = 0;
-          auto FV = [&](int k) -> double { return wv.F[k * 64 + lane]; };
-          for (int m = 0; m < (1 << L); ++m) {
-            if (!((act >> m) & 1u)) continue;
-            const TreeNode nd = tree_node(FV, lb, ub, se, L, m);
-            const Simp s = simp5(nd.ub - nd.lb, FV(nd.pos), FV(nd.pos + nd.W / 4),
-                                 FV(nd.pos + nd.W / 2), FV(nd.pos + 3 * nd.W / 4),
-                                 FV(nd.pos + nd.W));
-            if (simpson_refine(nd.S, s.S2, nd.err, depth - L, f)) nxt |= 3u << (2 * m);
-          }
-          if (L == kTreeDepth && nxt) f |= kFlagFallback;  // deeper than the in-wave levels
-          if (f) {
-            wv.fl[lane] |= f;
-            nxt = 0u;
-          }
-        }
-        if (COUNT && L == 0) prec = __popcll(__ballot(nxt != 0u));
-        if (L == kTreeDepth) break;
-        act = nxt;
-        // level L + 1's tasks, in lane order
-        int n = 0;
+      if (COUNT && L == 0 && tid < 64) ty.rec = __popcll(__ballot(need != 0u));
+      if (L == kTreeDepth) break;
+      if (tid == 0) {
+        cl.qn[0] = 0;
+        cl.qn[1] = 0;
+      }
+      team_sync<TW>();
+      // level L + 1's tasks: for each refining interval m of level L, the aux
+      // nodes d, e of both its halves (kAdaptZ: one grid per interval)
+      if (tid < 64) {
         if (MODE == kAdaptZ) {
           for (int m = 0; m < (1 << L); ++m)
-            n = wave_append((act >> (2 * m)) & 1u,
-                            lane | ((L == 0 ? kGridL1 : kGridL2L + m) << 11), wv.Q, n);
+            team_push((need >> m) & 1u, tid | ((L == 0 ? kGridL1 : kGridL2L + m) << 11), cl.Q,
+                      &cl.qn[0]);
         } else {
-          const int wc = kTreeW >> (L + 1);  // width of a level-(L + 1) interval
-          for (int k = 0; k < (2 << L); ++k)
-            for (int q = 1; q < 4; q += 2)
-              n = wave_append((act >> k) & 1u, lane | ((k * wc + q * (wc / 4)) << 6), wv.Q, n);
-        }
-        if (COUNT) {
-          if (L == 0) pq1 = n;
-          else pq2 = n;
-        }
-        nq = n;
-        wave_sync();
-        PHASE_MARK(4);
-        if (nq == 0) break;
-        ++L;
-        stage = 0;
-        r = 0;
-        nz = 0;
-        continue;
-      }
-      // ---- one round: at most one evaluation per lane ----
-      int owner = lane, pos = 0, gs = kGridRoot;
-      bool on;
-      if (stage == 0) {
-        const int e = r * 64 + lane;
-        on = e < nq;
-        if (on) {
-          const int code = wv.Q[e];
-          owner = code & 63;
-          pos = (code >> 6) & 31;
-          gs = code >> 11;
-        }
-      } else {
-        const int e = r * kZBatch + (lane >> 2);
-        on = e < nz;
-        gs = lane & 3;
-        if (on) {
-          const int code = wv.ZQ[e];
-          owner = code & 63;
-          pos = (code >> 6) & 31;
+          const int wm = kTreeW >> L;  // width of a level-L interval
+          for (int m = 0; m < (1 << L); ++m)
+            for (int q = 1; q < 8; q += 2)
+              team_push((need >> m) & 1u, tid | ((m * wm + q * (wm / 8)) << 6), cl.Q, &cl.qn[0]);
         }
       }
-      on = on && !(wv.fl[owner] & kFlagStop);
-      double y[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-      int flip = 0;
+      team_sync<TW>();
+      pc.mark(4);
+      if (COUNT) {
+        if (L == 0) ty.t1 = cl.qn[0];
+        else ty.t2 = cl.qn[0];
+      }
+      if (cl.qn[0] == 0) break;
+      ++L;
+      stage = 0;
+      r = 0;
+      continue;
+    }
+    // ---- one round: at most one evaluation per lane ----
+    int owner = tid & 63, pos = 0, gs = kGridRoot, zslot = 0;
+    bool on;
+    if (stage == 0) {
+      const int e = r * NT + tid;
+      on = e < nq;
       if (on) {
-        const double xo = wv.X[owner];
-        flip = xo > 0;
-        const double vo = flip ? -v : v;
-        const double xa = fabs(xo);
-        const double xx = (MODE == kAdaptZ) ? xa - t : xa - sh.tc[pos];
-        const TNode T = tnode_setup(xx, vo, sv, a, err);
-        if (T.amb) atomicOr(&wv.fl[owner], (int)kFlagExact);
-        if (MODE == kAdaptT) y[0] = tnode_pdf_sv(T, flip ? 1. - z : z, vo, sv, a);
-        else tnode_pdf_sv_grid5(T, sh.G[flip][gs], vo, sv, a, y);
+        const int code = cl.Q[e];
+        owner = code & 63;
+        pos = (code >> 6) & 31;
+        gs = code >> 11;
       }
-      if (stage == 0) {
-        bool pend = false;
-        if (on) {
-          if (MODE == kAdaptT) {
-            wv.F[pos * 64 + owner] = y[0] * iw;
-            if (COUNT) atomicAdd(&wv.cnt[owner], 1);
-          } else if (MODE == kAdaptZ) {
-            const double izf = sh.iz[flip];
-#pragma unroll
-            for (int j = 0; j < 5; ++j)
-              if (grid_owns(gs, j)) wv.F[grid_point(gs, j) * 64 + owner] = y[j] * izf;
-            if (COUNT) atomicAdd(&wv.cnt[owner], 4);
-          } else {
-            // kAdaptTZ: the z integral's prologue + root test (integrate.pxi:
-            // 114-141); a refinement queues the z walk
-            const double izf = sh.iz[flip];
-            const Simp s = simp5(sh.hz[flip], y[0] * izf, y[1] * izf, y[2] * izf, y[3] * izf,
-                                 y[4] * izf);
-            int f = 0;
-            pend = simpson_refine(s.S, s.S2, se, nsz, f);
-            if (f) atomicOr(&wv.fl[owner], f);
-            else if (!pend) wv.F[pos * 64 + owner] = (s.S2 + (s.S2 - s.S) / 15) * iw;
-            if (COUNT) atomicAdd(&wv.cnt[owner], 5);
-          }
-        }
-        if (MODE == kAdaptTZ) nz = wave_append(pend && on, owner | (pos << 6), wv.ZQ, nz);
-      } else if (MODE == kAdaptTZ) {
-        if (on) {
-          const double izf = sh.iz[flip];
-          double* zv = wv.ZV + (lane >> 2) * kTreePoints;
+    } else {
+      zslot = tid >> 2;
+      const int e = r * 16 * TW + zslot;
+      on = e < nz;
+      gs = tid & 3;
+      if (on) {
+        const int code = cl.ZQ[e];
+        owner = code & 63;
+        pos = (code >> 6) & 31;
+      }
+    }
+    on = on && !(cl.fl[owner] & kFlagStop);
+    double y[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    int flip = 0;
+    if (on) {
+      const double xo = cl.X[owner];
+      flip = xo > 0;
+      const double vo = flip ? -v : v;
+      const double xa = fabs(xo);
+      const double xx = (MODE == kAdaptZ) ? xa - t : xa - cl.tab.tP[pos];
+      // level-0 t nodes (split units): the per-lane loop's hints (l0_hints)
+      double qh = -1.0;
+      bool known = false;
+      Decision kd{0, 0, 0};
+      if (MODE != kAdaptZ && L == 0 && stage == 0) {
+        const L0Hints H = l0_hints(xa, cl.tab.tP[0], cl.tab.tP[kTreeW], a, err);
+        const int j = pos / (kTreeW / 4);
+        qh = j == 0 ? H.qn[0] : j == 1 ? H.qn[1] : j == 2 ? H.qn[2] : j == 3 ? H.qn[3] : H.qn[4];
+        known = j == 0 ? H.ok0 : (j == 4 ? H.ok4 : H.shared);
+        kd = j == 4 ? H.D4 : H.D0;
+      }
+      const TNode T = tnode_setup(xx, vo, sv, a, err, qh, known, kd);
+      if (T.amb) atomicOr(&cl.fl[owner], (int)kFlagExact);
+      if (MODE == kAdaptT) y[0] = tnode_pdf_sv(T, flip ? 1. - z : z, vo, sv, a);
+      else tnode_pdf_sv_grid5(T, cl.tab.G[flip][gs], vo, sv, a, y);
+    }
+    if (stage == 0) {
+      bool pend = false;
+      if (on) {
+        if (MODE == kAdaptT) {
+          cl.F[pos * 64 + owner] = y[0] * iwt;
+          if (COUNT) atomicAdd(&cl.cnt[owner], 1);
+        } else if (MODE == kAdaptZ) {
+          const double izf = cl.tab.iz[flip];
 #pragma unroll
           for (int j = 0; j < 5; ++j)
-            if (grid_owns(gs, j)) zv[grid_point(gs, j)] = y[j] * izf;
-        }
-        wave_sync();
-        const int e = r * kZBatch + lane;
-        if (lane < kZBatch && e < nz) {
-          const int code = wv.ZQ[e];
-          const int ow = code & 63, ps = (code >> 6) & 31;
-          if (!(wv.fl[ow] & kFlagStop)) {
-            const int fz = wv.X[ow] > 0;
-            const double* zv = wv.ZV + lane * kTreePoints;
-            int f = 0, nref = 0;
-            const double zi = tree_value([&](int k) -> double { return zv[k]; }, sh.lbz[fz],
-                                         sh.ubz[fz], se, nsz, f, nref);
-            if (f) atomicOr(&wv.fl[ow], f);
-            else wv.F[ps * 64 + ow] = zi * iw;
-            if (COUNT) atomicAdd(&wv.cnt[ow], 4 * nref);
-          }
+            if (grid_owns(gs, j)) cl.F[grid_point(gs, j) * 64 + owner] = y[j] * izf;
+          if (COUNT) atomicAdd(&cl.cnt[owner], gs == kGridRoot ? 5 : 4);
+        } else {
+          // kAdaptTZ: the z integral's prologue + root test (integrate.pxi:
+          // 114-141); a refinement queues the z walk
+          const double izf = cl.tab.iz[flip];
+          const double hz = cl.tab.zP[flip][kTreeW] - cl.tab.zP[flip][0];
+          const Simp s = simp5(hz, y[0] * izf, y[1] * izf, y[2] * izf, y[3] * izf, y[4] * izf);
+          int f = 0;
+          pend = simpson_refine(s.S, s.S2, se, nsz, f);
+          if (f) atomicOr(&cl.fl[owner], f);
+          else if (!pend) cl.F[pos * 64 + owner] = (s.S2 + (s.S2 - s.S) / 15) * iwt;
+          if (COUNT) atomicAdd(&cl.cnt[owner], 5);
         }
       }
-      ++r;
-      wave_sync();
-      if (stage == 0) PHASE_MARK(3);
+      if (MODE == kAdaptTZ) team_push(pend && on, owner | (pos << 6), cl.ZQ, &cl.qn[1]);
+      ++pc.nt;
+    } else if (MODE == kAdaptTZ) {
+      if (on) {
+        const double izf = cl.tab.iz[flip];
+        double* zv = cl.ZV + zslot * kTreePoints;
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (grid_owns(gs, j)) zv[grid_point(gs, j)] = y[j] * izf;
+      }
+      team_sync<TW>();
+      const int e = r * 16 * TW + tid;
+      if (tid < 16 * TW && e < nz) {
+        const int code = cl.ZQ[e];
+        const int ow = code & 63, ps = (code >> 6) & 31;
+        if (!(cl.fl[ow] & kFlagStop)) {
+          double zv[kTreePoints];
+#pragma unroll
+          for (int k = 0; k < kTreePoints; ++k) zv[k] = cl.ZV[tid * kTreePoints + k];
+          int f = 0, nref = 0;
+          unsigned need = 0u;
+          const double zi = tree17(zv, cl.tab.zP[cl.X[ow] > 0], se, nsz, kTreeDepth, f, need, nref);
+          if (need) f |= kFlagFallback;  // z tree deeper than the walk's levels
+          if (f & (kFlagExact | kFlagFallback)) atomicOr(&cl.fl[ow], f & (kFlagExact | kFlagFallback));
+          else cl.F[ps * 64 + ow] = zi * iwt;
+          if (COUNT) atomicAdd(&cl.cnt[ow], 4 * nref);
+        }
+      }
+      ++pc.nz;
     }
-    wave_sync();
+    ++r;
+    team_sync<TW>();
+    if (stage == 0) pc.mark(3);
   }
-  // ---- the own trial: its density (level 0, or its tree's value: the
-  // reference's recursion over the stored values), or a deferred slot ----
-  bool defer = oc == kExact;
-  int rf = kFlagExact;
-  if (oc == kTree) {
-    const int ff = wv.fl[lane];
-    if (ff & (kFlagExact | kFlagFallback)) {
-      defer = true;
-      rf = (ff & kFlagExact) ? kFlagExact : kFlagFallback;
-    } else {
-      int f = 0, nref = 0;
-      p = tree_value([&](int k) -> double { return wv.F[k * 64 + lane]; }, lb, ub, se, depth, f,
-                     nref);
-      // structural zero: no evaluation point with x - t_node > 0
-      const bool structural = (MODE == kAdaptZ) ? tr.x - t <= 0 : tr.x - lb <= 0;
-      defer = (f & (kFlagExact | kFlagFallback)) || !(p > kExactBelow || structural);
-    }
+}
+
+// Final density of owner lane o (a refined tree: tree17 over its stored
+// values; the level tests already flagged ties and deeper trees).
+template <int MODE, int TW>
+__device__ inline void tree_density(const TrialArgs& A, const ChunkLds<TW>& cl, int o, double x,
+                                    double& p, bool& defer, int& rf) {
+  const int ff = cl.fl[o];
+  if (ff & (kFlagExact | kFlagFallback)) {
+    defer = true;
+    rf = (ff & kFlagExact) ? kFlagExact : kFlagFallback;
+    return;
   }
+  double f[kTreePoints];
+  load_tree(cl, o, f);
+  const Trial tr = trial_setup(x, A.P);
+  const double(&P)[kTreePoints] = (MODE == kAdaptZ) ? cl.tab.zP[x > 0] : cl.tab.tP;
+  const int depth = (MODE == kAdaptZ) ? A.K.n_sz : A.K.n_st;
+  int fl = 0, nref = 0;
+  unsigned need = 0u;
+  p = tree17(f, P, A.K.simps_err, depth, kTreeDepth, fl, need, nref);
+  // structural zero: no evaluation point with x - t_node > 0
+  const bool structural = (MODE == kAdaptZ) ? tr.x - A.P.t <= 0 : tr.x - P[0] <= 0;
+  defer = (fl & kFlagExact) || need || !(p > kExactBelow || structural);
+  rf = kFlagExact;
+}
+
+// Chunk outputs of the owner lanes (one wave): per-trial emit, deferred
+// slots, the chunk partial and the evaluation count.
+template <bool COUNT, int OUT>
+__device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, int lane, double p,
+                                 bool defer, int rf, long long ne) {
+  const int64_t i = c * 64 + lane;
   double lp = 0.0;
   int zero = 0;
   if (i < A.n && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
-  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
   defer_slots(W, c, lane, defer, rf);
   if (OUT == OUT_SUM) {
     lp = wave_sum(lp);
@@ -512,25 +530,196 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
       A.zeros[c] = zs;
     }
   }
-#ifdef WFPT_PHASE_TIMING
-  PHASE_MARK(4);
-  if (lane == 0)
-    for (int k = 0; k < 5; ++k) atomicAdd(&W.prof[11 + k], (int)(ph[k] >> 10));
-#endif
   if (COUNT) {
-    const long long nf = wave_sum_ll((i < A.n && !defer) ? (long long)wv.cnt[lane] : 0ll);
-    if (lane == 0) {
-      atomicAdd(A.evals, (unsigned long long)nf);
-      // wfpt_profile_lists
-      atomicAdd(&W.prof[1], pq1);
-      atomicAdd(&W.prof[2], pq2);
-      atomicAdd(&W.prof[4], prec);
-      atomicAdd(&W.prof[7], pz0 + pz1 + pz2);
-      atomicAdd(&W.prof[8], pz0);
-      atomicAdd(&W.prof[9], pz1);
-      atomicAdd(&W.prof[10], pz2);
+    const long long nf = wave_sum_ll((i < A.n && !defer) ? ne : 0ll);
+    if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
+  }
+}
+
+__device__ inline void tally_out(const Work& W, const Tally& ty) {
+  atomicAdd(&W.prof[1], ty.t1);
+  atomicAdd(&W.prof[2], ty.t2);
+  atomicAdd(&W.prof[4], ty.rec);
+  atomicAdd(&W.prof[7], ty.z[0] + ty.z[1] + ty.z[2]);
+  atomicAdd(&W.prof[8], ty.z[0]);
+  atomicAdd(&W.prof[9], ty.z[1]);
+  atomicAdd(&W.prof[10], ty.z[2]);
+}
+
+// Records chunk c for the next call's split (lane 0 of its last wave).
+__device__ inline void record_heavy(const Split& S, int64_t c, bool heavy) {
+  if (!S.next_pred) return;
+  unsigned char flag = 0;
+  if (heavy) {
+    const int slot = atomicAdd(S.next_n, 1);
+    if (slot < S.cap) {
+      S.next_list[slot] = (int)c;
+      flag = 1;
     }
   }
+  S.next_pred[c] = flag;
+}
+
+// Chunk outputs of a split unit's trials: per-trial outputs now, the chunk
+// partial's terms to S.lp / S.meta; the chunk's last unit (agent-scope
+// release / acquire hand-off) folds them in wave_sum's order and writes the
+// chunk's deferred slots in lane order, exactly as an unsplit chunk's wave.
+template <int MODE, bool COUNT, int OUT>
+__device__ inline void split_out(const TrialArgs& A, const Work& W, const Split& S,
+                                 const ChunkLds<1>& cl, int slot, int sub, int lane, double x0,
+                                 int nz0) {
+  const int64_t c = S.list[slot];
+  const int64_t i = c * 64 + sub * kSplitTrials + lane;
+  const bool own = lane < kSplitTrials && i < A.n;
+  double p = 0.0, lp = 0.0;
+  bool defer = false;
+  int rf = kFlagExact, zero = 0;
+  if (own && !(cl.fl[lane] & kFlagIdle)) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+  if (own && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
+  if (lane < kSplitTrials) {
+    const int k = slot * 64 + sub * kSplitTrials + lane;
+    S.lp[k] = lp;
+    S.meta[k] = zero | ((int)defer << 1) | (rf << 2);
+  }
+  if (COUNT) {
+    const long long nf = wave_sum_ll((own && !defer) ? (long long)cl.cnt[lane] : 0ll);
+    if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  int prev = 0;
+  if (lane == 0) {
+    atomicAdd(&S.zn[slot], nz0);
+    prev = __hip_atomic_fetch_add(&S.done[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  prev = __shfl(prev, 0, 64);
+  if (prev != kSplit - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const double lpc = S.lp[slot * 64 + lane];
+  const int m = S.meta[slot * 64 + lane];
+  defer_slots(W, c, lane, (m >> 1) & 1, m >> 2);
+  if (OUT == OUT_SUM) {
+    const double sum = wave_sum(lpc);
+    const int zs = __popcll(__ballot((m & 1) != 0));
+    if (lane == 0) {
+      A.out[c] = sum;
+      A.zeros[c] = zs;
+    }
+  }
+  if (lane == 0) {
+    const int znc = __hip_atomic_load(&S.zn[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    record_heavy(S, c, znc > kHeavyZ);
+    S.done[slot] = 0;
+    S.zn[slot] = 0;
+  }
+}
+
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work W, EngTables tab,
+                                                              Split S) {
+  __shared__ ChunkLds<1> lds[kEngWaves];
+  const int lane = threadIdx.x & 63;
+  ChunkLds<1>& cl = lds[threadIdx.x >> 6];
+  PhaseClock pc;
+  pc.start();
+#ifdef WFPT_PHASE_TIMING
+  const long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+  load_tables(cl, tab, lane);
+  // work units: the split chunks' units first (dispatched first), then one
+  // wave per chunk
+  const int64_t u = (int64_t)blockIdx.x * kEngWaves + (threadIdx.x >> 6);
+  const bool split = u < (int64_t)S.n * kSplit;
+  const int slot = split ? (int)(u / kSplit) : 0, sub = split ? (int)(u % kSplit) : 0;
+  const int64_t c = split ? (int64_t)S.list[slot] : u - (int64_t)S.n * kSplit;
+  if (!split && (c * 64 >= A.n || (S.n > 0 && S.pred[c]))) return;  // past the end / split
+  const int64_t i = split ? c * 64 + sub * kSplitTrials + lane : c * 64 + lane;
+  const bool own = (split ? lane < kSplitTrials : true) && i < A.n;
+  const double x0 = own ? A.x[i] : 0.0;
+  wave_sync();
+  double p = 0.0;
+  long long ne0 = 0;
+  int oc = kFinal, stage = 1;
+  bool rounds;
+  if (!split) {
+    // ---- level 0, each lane its own trial, in registers ----
+    double f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    unsigned pend0 = 0u;
+    if (own) {
+      const ZGrid G = cl.tab.G[x0 > 0][kGridRoot];
+      oc = eng_level0<MODE>(x0, A.P, A.K, G, p, f0, ne0, pend0);
+    }
+    pc.mark(0);
+    rounds = __ballot(oc == kTree) != 0ull;
+    if (rounds) {
+      cl.X[lane] = x0;
+      cl.fl[lane] = oc == kTree ? 0 : (oc == kExact ? (int)kFlagExact : (int)kFlagIdle);
+      if (COUNT) cl.cnt[lane] = (int)ne0;
+      if (oc == kTree) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) cl.F[j * (kTreeW / 4) * 64 + lane] = f0[j];
+      }
+      if (lane == 0) {
+        cl.qn[0] = 0;
+        cl.qn[1] = 0;
+      }
+      wave_sync();
+      // the pending z integrals of the refining trials (kAdaptTZ)
+      if (MODE == kAdaptTZ) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          team_push(oc == kTree && ((pend0 >> (j * (kTreeW / 4))) & 1u),
+                    lane | ((j * (kTreeW / 4)) << 6), cl.ZQ, &cl.qn[1]);
+      }
+    }
+  } else {
+    // ---- a split unit: its kSplitTrials trials' level 0 as tasks (t node j
+    // of owner o, or owner o's root z grid) ----
+    cl.X[lane] = x0;
+    cl.fl[lane] = (own && trial_setup(x0, A.P).valid) ? 0 : kFlagIdle;
+    if (COUNT) cl.cnt[lane] = 0;
+    if (lane == 0) {
+      cl.qn[0] = 0;
+      cl.qn[1] = 0;
+    }
+    wave_sync();
+    constexpr int n0 = (MODE == kAdaptZ) ? 1 : 5;
+    const int o = lane % kSplitTrials, j = lane / kSplitTrials;
+    team_push(j < n0 && !(cl.fl[o] & kFlagStop), o | ((j * (kTreeW / 4)) << 6), cl.Q, &cl.qn[0]);
+    stage = 0;
+    rounds = true;
+  }
+  Tally ty;
+  int nz0 = 0;
+  if (rounds) {
+    wave_sync();
+    nz0 = cl.qn[1];
+    pc.mark(1);
+    refine_rounds<MODE, COUNT, 1>(A, cl, lane, stage, ty, pc);
+    if (split) nz0 = ty.z[0];
+  }
+  if (split) {
+    split_out<MODE, COUNT, OUT>(A, W, S, cl, slot, sub, lane, x0, nz0);
+    if (COUNT && lane == 0) tally_out(W, ty);
+    return;
+  }
+  if (lane == 0) record_heavy(S, c, nz0 > kHeavyZ);
+  bool defer = oc == kExact;
+  int rf = kFlagExact;
+  if (oc == kTree) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, defer, rf, oc == kTree ? (long long)cl.cnt[lane] : ne0);
+  pc.mark(4);
+#ifdef WFPT_PHASE_TIMING
+  if (lane == 0 && c < kPhaseWaves) {
+    unsigned long long* rec = W.phase + c * 8;
+    rec[0] = rt0;
+    rec[1] = __builtin_amdgcn_s_memrealtime();
+    for (int k = 0; k < 5; ++k) rec[2 + k] = pc.ph[k];
+    rec[7] = (unsigned long long)pc.nz | ((unsigned long long)pc.nt << 32);
+  }
+#endif
+  if (COUNT && lane == 0) tally_out(W, ty);
 }
 
 // Settles every deferred trial and folds it into its chunk: block g walks
@@ -622,7 +811,8 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
                                                         int64_t nb, const int* wl_n, int64_t nw,
                                                         int* status, double* out,
-                                                        unsigned long long seq) {
+                                                        unsigned long long seq,
+                                                        const int* split_rd, int* split_rs) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
   __shared__ int sd[16];
@@ -669,6 +859,9 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     out[1] = (double)zz;
     out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
     out[3] = (double)dd;
+    // heavy chunks recorded for the next call (Split)
+    out[5] = split_rd ? (double)*split_rd : 0.0;
+    if (split_rs) *split_rs = 0;
     __threadfence_system();
     // completion word, written after the results are visible: the host may
     // poll it instead of waiting on the stream
@@ -686,6 +879,7 @@ __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* 
     out[1] = res[1];
     out[2] = res[2];
     out[3] = 0.0;
+    out[5] = res[5];
     __threadfence_system();
     reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
     __threadfence_system();
@@ -947,13 +1141,17 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
 }
 
 template <int MODE, bool COUNT, int OUT>
-static void run_fast(const TrialArgs& A, const Work& W, hipStream_t s, hipEvent_t fast_done) {
-  if constexpr (MODE == kDirect)
+static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
+                     hipStream_t s, hipEvent_t fast_done) {
+  if constexpr (MODE == kDirect) {
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W);
-  else
-    hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>), dim3((A.n + kEngBlock - 1) / kEngBlock),
-                       dim3(kEngBlock), 0, s, A, W);
+  } else {
+    const int64_t units = (int64_t)S.n * kSplit + (A.n + 63) / 64;
+    hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>),
+                       dim3((units + kEngWaves - 1) / kEngWaves), dim3(kEngBlock), 0, s, A, W, T,
+                       S);
+  }
   if (fast_done) (void)hipEventRecord(fast_done, s);
 }
 
@@ -966,11 +1164,13 @@ static void run_deferred(const TrialArgs& A, const Work& W, hipStream_t s) {
 }
 
 template <bool COUNT, int OUT>
-static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W,
+static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, const Split& S,
                         hipStream_t s, hipEvent_t fast_done) {
+  EngTables T;
+  if (mode >= kAdaptT && mode <= kAdaptTZ) eng_tables(A.P, T);
 #define FAST_AND_DEFERRED(M_)                                               \
   do {                                                                      \
-    if (part & kPassFast) run_fast<M_, COUNT, OUT>(A, W, s, fast_done);     \
+    if (part & kPassFast) run_fast<M_, COUNT, OUT>(A, W, T, S, s, fast_done); \
     if (part & kPassDeferred) run_deferred<M_, COUNT, OUT>(A, W, s);        \
   } while (0)
   switch (mode) {
@@ -1005,27 +1205,31 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
 
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
-                   int logp, const Work& W, hipStream_t s, hipEvent_t fast_done) {
+                   int logp, const Work& W, hipStream_t s, hipEvent_t fast_done,
+                   const Split* split) {
   if (n <= 0) return;
+  Split S{};
+  if (split) S = *split;
   const TrialArgs A = trial_args(x, n, P, K, out, zeros, evals, status, logp);
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   if (evals) {
-    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, s, fast_done);
+    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, S, s, fast_done);
     else if (out_kind == OUT_ARRAY)
-      launch_mode<true, OUT_ARRAY>(mode, part, A, W, s, fast_done);
-    else launch_mode<true, OUT_LOGP>(mode, part, A, W, s, fast_done);
+      launch_mode<true, OUT_ARRAY>(mode, part, A, W, S, s, fast_done);
+    else launch_mode<true, OUT_LOGP>(mode, part, A, W, S, s, fast_done);
   } else {
-    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, s, fast_done);
+    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, S, s, fast_done);
     else if (out_kind == OUT_ARRAY)
-      launch_mode<false, OUT_ARRAY>(mode, part, A, W, s, fast_done);
-    else launch_mode<false, OUT_LOGP>(mode, part, A, W, s, fast_done);
+      launch_mode<false, OUT_ARRAY>(mode, part, A, W, S, s, fast_done);
+    else launch_mode<false, OUT_LOGP>(mode, part, A, W, S, s, fast_done);
   }
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
-                     int* status, double* out, unsigned long long seq, hipStream_t s) {
+                     int* status, double* out, unsigned long long seq, hipStream_t s,
+                     const int* split_rd, int* split_rs) {
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, wl_n, nw, status,
-                     out, seq);
+                     out, seq, split_rd, split_rs);
 }
 
 template <int MODE, bool COUNT>

@@ -160,6 +160,10 @@ int wfpt_profile_read(wfpt_ctx *ctx, double *kernel_ms, int64_t *launches, int64
  * level L). counts[11..15]: per-phase engine time of diagnostic builds
  * (WFPT_PHASE_TIMING), kilo-cycles summed over waves. */
 int wfpt_profile_lists(wfpt_ctx *ctx, int64_t counts[16], int reset);
+/* Diagnostic builds (WFPT_PHASE_TIMING): the last engine launch's per-wave
+ * records, 8 words per 64-trial chunk {start, end (100 MHz real-time clock),
+ * 5 phase cycle counts, z rounds | t rounds << 32}; zeros otherwise. */
+int wfpt_debug_waves(wfpt_ctx *ctx, uint64_t *out, int64_t max_records);
 int wfpt_synchronize(wfpt_ctx *ctx);
 
 #ifdef __cplusplus
