@@ -8,8 +8,8 @@ Restates hddm/likelihoods.py:30-105 (`generate_wfpt_stochastic_class`,
   branch (|rt| >= 999 scored by a binomial on P(upper), likelihoods.py:56-73).
 * The observed data of a node never changes during sampling, so the RT
   column is uploaded once per node and kept resident (`Dataset`), keyed by the
-  identity and contents of the node's value; the reference re-reads host
-  memory on every logp call.
+  identity of the node's value (contents hashed only on a miss); the
+  reference re-reads host memory on every logp call.
 * `generate_wfpt_stochastic_class` returns the same PyMC class as the
   reference when kabuki is importable (kabuki.utils.stochastic_from_dist);
   otherwise a light `WfptNode` with `.value`, `.parents`, `.logp`, `.pdf`,
@@ -35,22 +35,48 @@ def _rt_column(x):
 
 
 class _ResidentCache:
-    """Device-resident copies of node data keyed by their exact bytes (a node's
-    RT column never changes during sampling; changed data is a new key)."""
+    """Device-resident copies of node data (a node's RT column never changes
+    during sampling; changed data is a new entry).
+
+    A logp call must not pay an O(n) host pass in front of a ~0.15 ms kernel,
+    so lookups are keyed on the column's identity (buffer address, length and
+    the node's value object, which the entry keeps alive so neither can be
+    recycled while the entry exists). Contents are hashed only on a miss (nodes
+    holding equal data share one upload); a hit re-checks a 64-element sample
+    of the column so an in-place rewrite of a node's value is not served stale.
+    Each entry also caches max|rt| for wfpt_like's `< 998` dispatch."""
 
     def __init__(self, maxsize=4096):
-        self._d = {}
+        self._by_id = {}
+        self._by_bytes = {}
         self.maxsize = maxsize
 
-    def get(self, rt):
-        key = rt.tobytes()
-        ds = self._d.get(key)
-        if ds is None:
-            if len(self._d) >= self.maxsize:
-                self._d.clear()
-            ds = _wfpt.Dataset(rt)
-            self._d[key] = ds
-        return ds
+    @staticmethod
+    def _probe(rt):
+        return rt[:: max(1, rt.size // 64)][:64].copy()
+
+    def get(self, rt, src):
+        """(Dataset or None, max|rt|) for the contiguous column `rt` of `src`.
+        The Dataset is None when the column holds missing responses."""
+        key = (rt.ctypes.data, rt.size, id(src))
+        hit = self._by_id.get(key)
+        if hit is not None and hit[0] is src and np.array_equal(hit[1], self._probe(rt)):
+            return hit[2], hit[3]
+        if len(self._by_id) >= self.maxsize:
+            self._by_id.clear()
+            self._by_bytes.clear()
+        bkey = rt.tobytes()
+        ent = self._by_bytes.get(bkey)
+        if ent is None:
+            amax = float(np.abs(rt).max(initial=0.0))
+            ent = (_wfpt.Dataset(rt) if rt.size and amax < 998 else None, amax)
+            self._by_bytes[bkey] = ent
+        self._by_id[key] = (src, self._probe(rt)) + ent
+        return ent
+
+    def clear(self):
+        self._by_id.clear()
+        self._by_bytes.clear()
 
 
 _cache = _ResidentCache()
@@ -62,10 +88,13 @@ def make_wfpt_like(wiener_params=None, resident=True):
 
     def wfpt_like(x, v, sv, a, z, sz, t, st, p_outlier=0):
         rt = np.ascontiguousarray(_rt_column(x))
-        if np.abs(rt).max(initial=0.0) < 998:
-            if resident and rt.size:
-                return _cache.get(rt).wiener_like(v, sv, a, z, sz, t, st, p_outlier=p_outlier,
-                                                  **wp)
+        if resident:
+            ds, amax = _cache.get(rt, x)
+        else:
+            ds, amax = None, float(np.abs(rt).max(initial=0.0))
+        if amax < 998:
+            if ds is not None:
+                return ds.wiener_like(v, sv, a, z, sz, t, st, p_outlier=p_outlier, **wp)
             return _wfpt.wiener_like(rt, v, sv, a, z, sz, t, st, p_outlier=p_outlier, **wp)
         # missing responses (currently undocumented in the reference)
         noresponse = np.abs(rt) >= 999
@@ -82,6 +111,34 @@ def make_wfpt_like(wiener_params=None, resident=True):
 
     wfpt_like.wiener_params = wp
     return wfpt_like
+
+
+def gen_random(parents, size, sampling_method="cdf", cdf_range=(-5, 5), sampling_dt=1e-4):
+    """The class's `random` (likelihoods.py:76-81): hddm.generate.gen_rts
+    (generate.py:134-205, structured=True) followed by hddm.utils.flip_errors
+    (utils.py:15-37), i.e. a DataFrame with signed 'rt' and 'response'
+    (1 upper / 0 lower). method 'cdf' samples on the MI355X density grid
+    (gen_rts_from_cdf); the host-only simulators ('drift', 'cdf_py') are the
+    reference's own and are delegated to it when it is importable."""
+    import pandas as pd
+    p = {k: parents[k] for k in ("v", "sv", "a", "z", "sz", "t", "st") if k in parents}
+    for k in ("sv", "sz", "st"):        # generate.py:169-177 defaults
+        p.setdefault(k, 0)
+    p.setdefault("z", .5)
+    if isinstance(size, tuple):         # generate.py:180-184 (PyMC shapes)
+        size = 1 if size == () else size[0]
+    if sampling_method != "cdf":
+        import hddm  # reference simulators (not on the accelerated path)
+        return hddm.utils.flip_errors(hddm.generate.gen_rts(
+            method=sampling_method, size=size, dt=sampling_dt, range_=cdf_range,
+            structured=True, **parents))
+    rts = _wfpt.gen_rts_from_cdf(p["v"], p["sv"], p["a"], p["z"], p["sz"], p["t"], p["st"],
+                                 size, cdf_range[0], cdf_range[1], sampling_dt)
+    # generate.py:200-203 then utils.py:27-35: |rt| with response, lower flipped back
+    response = np.where(rts < 0, 0.0, 1.0)
+    rt = np.abs(rts)
+    rt = np.where(response == 0, -rt, rt)
+    return pd.DataFrame({"rt": rt, "response": response})
 
 
 class WfptNode:
@@ -120,12 +177,14 @@ class WfptNode:
         return _cdfdif.dmat_cdf_array(np.ascontiguousarray(x, dtype=np.float64),
                                       w_outlier=self._like.wiener_params["w_outlier"], **pv)
 
-    def random(self, size=None):
-        pv = self.parent_values()
-        n = size or len(_rt_column(self.value))
-        return _wfpt.gen_rts_from_cdf(pv["v"], pv["sv"], pv["a"], pv["z"], pv["sz"], pv["t"],
-                                      pv["st"], samples=n, cdf_lb=self.cdf_range[0],
-                                      cdf_ub=self.cdf_range[1], dt=self.sampling_dt)
+    @property
+    def shape(self):
+        return np.shape(_rt_column(self.value))
+
+    def random(self):
+        """likelihoods.py:76-81: a DataFrame of len(value) signed RTs + responses."""
+        return gen_random(self.parent_values(), self.shape, self.sampling_method,
+                          self.cdf_range, self.sampling_dt)
 
 
 def generate_wfpt_stochastic_class(wiener_params=None, sampling_method="cdf",
@@ -152,6 +211,11 @@ def generate_wfpt_stochastic_class(wiener_params=None, sampling_method="cdf",
         return _cdfdif.dmat_cdf_array(x, w_outlier=wfpt_like.wiener_params["w_outlier"],
                                       **self.parents)
 
+    def random(self):
+        return gen_random(self.parents.value, self.shape, sampling_method, cdf_range,
+                          sampling_dt)
+
     wfpt_cls.pdf = pdf
     wfpt_cls.cdf = cdf
+    wfpt_cls.random = random
     return wfpt_cls
