@@ -109,6 +109,8 @@ struct wfpt_ctx {
   DevBuf<unsigned char> wl;  // lane of the deferred trial in each slot
   DevBuf<int> wl_n;          // per chunk: deferred trials
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
+  DevBuf<unsigned char> redo;  // per chunk: the lean pass left it to the engine (0 at rest)
+  int* tree_any = nullptr;   // device: some chunk refined in-wave (finalize reports + clears)
   int* prof = nullptr;       // device: 16 refinement work counters (PROF_EVALS)
   unsigned long long* phase = nullptr;  // device: engine phase cycles (diagnostic builds)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
@@ -126,6 +128,7 @@ struct wfpt_ctx {
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
+  bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
   double k_ms = 0.0;
@@ -148,6 +151,9 @@ struct wfpt_ds {
   // the last call on this dataset deferred no trial: the next one runs the
   // level-0 pass + finalize only (run_sum_fast), no slow pass
   mutable bool no_defer = false;
+  // the last call on this dataset refined no chunk in-wave: the next one's
+  // level-0 pass is the lean kernel (kPassLean)
+  mutable bool no_tree = false;
   // heavy-chunk record (wfpt_internal.h: Split), double-buffered by call
   // parity: the engine writes [1 - parity] while it reads [parity]
   int64_t nw = 0;
@@ -231,6 +237,12 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   HIP_TRY(c->wl.reserve(ns));
   HIP_TRY(c->wl_n.reserve(nw));
   HIP_TRY(c->rflag.reserve(ns));
+  if (c->redo.cap < (size_t)nw) {
+    HIP_TRY(c->redo.reserve(nw));
+    HIP_TRY(hipMemsetAsync(c->redo.p, 0, c->redo.cap, c->stream));
+  }
+  W->redo = c->redo.p;
+  W->tree_any = c->tree_any;
   W->wl = c->wl.p;
   W->wl_n = c->wl_n.p;
   W->rflag = c->rflag.p;
@@ -314,7 +326,10 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   // the one rocprofv3 reports as fast_kernel<...>)
   const bool prof = c->profile && (part & wfpt::kPassFast);
   if (prof) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  const bool eng = d && d->hcount && engine_family(P, K);
+  // heavy-chunk splitting belongs to full engine calls (not the lean / redo
+  // passes)
+  const bool eng = d && d->hcount && engine_family(P, K) &&
+                   !(part & (wfpt::kPassLean | wfpt::kPassRedo));
   const wfpt::Split S = eng ? split_of(d) : wfpt::Split{};
   wfpt::launch_trials(0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p, c->zero.p,
                       c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
@@ -323,7 +338,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   const int64_t nw = (n + 63) / 64;
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? W.wl_n : nullptr, adaptive ? nw : 0,
                         c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
-                        eng ? d->hcount + d->parity : nullptr);
+                        eng ? d->hcount + d->parity : nullptr, c->tree_any);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -382,8 +397,10 @@ int wait_result(wfpt_ctx* c, const double* r) {
 
 // Decodes {sum, zeros, errors, deferred} from host memory `r` of a finished
 // call; *deferred (if given) = the level-0 pass deferred trials.
+bool res_deferred(const double* r) { return ((int)r[3] & wfpt::kResDeferred) != 0; }
+bool res_tree(const double* r) { return ((int)r[3] & wfpt::kResTree) != 0; }
 int decode_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr) {
-  if (deferred) *deferred = r[3] != 0.0;
+  if (deferred) *deferred = res_deferred(r);
   if (int rc = wfpt_decode_result(r, out)) return rc;
   return finish_profile(c);
 }
@@ -394,29 +411,55 @@ int read_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr
   return decode_sum(c, r, out, deferred);
 }
 
-// Resident-data sum predicted to defer nothing (the dataset's last call did
-// not): level-0 pass + finalize only (no deferred-trial kernels). If the pass
-// did defer trials this time (finalize reports it), the deferred pass and a
-// second finalize run over the intact chunk partials, giving the same result
-// bit for bit as the full sequence; only that call pays a host round trip.
-// Returns -1 when the path does not apply (nothing launched).
+// Waits for a resident call, updates the dataset's predictions from its
+// result and decodes it.
+int finish_sum(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
+               double* out, bool lean) {
+  if (int rc = wait_result(c, c->mres)) return rc;
+  const bool eng = engine_family(P, K);
+  split_advance(d, eng && !lean, c->mres);
+  bool deferred = true;
+  const int rc = decode_sum(c, c->mres, out, &deferred);
+  if (rc == WFPT_OK) {
+    d->no_defer = c->fast_only && !deferred;
+    if (eng) d->no_tree = !res_tree(c->mres);
+  }
+  return rc;
+}
+
+// Resident-data sums with a predicted call sequence (from the dataset's last
+// call), each giving the full sequence's result bit for bit:
+//   * no deferred trial predicted: level-0 pass + finalize only (no fold
+//     launch). If the pass did defer this time (finalize reports it), the
+//     deferred pass and a second finalize run over the intact chunk partials;
+//     only that call pays a host round trip.
+//   * no in-wave refinement predicted (engine families): the level-0 pass is
+//     the lean kernel; chunks that do refine are flagged and the engine's redo
+//     pass processes them before the fold (as part of the deferred pass).
+// Returns -1 when neither prediction applies (nothing launched).
 int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
                  double* out) {
   const int64_t n = d->n;
-  if (c->count || !d->no_defer || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
+  if (c->count || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
   const bool eng = engine_family(P, K);
-  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassFast, d)) return rc;
-  if (int rc = wait_result(c, c->mres)) return rc;
-  if (c->mres[3] == 0.0) {
-    split_advance(d, eng, c->mres);
-    return decode_sum(c, c->mres, out);
+  const bool lean = eng && c->lean && d->no_tree;
+  const bool fast = c->fast_only && d->no_defer;
+  if (!lean && !fast) return -1;
+  const int lp = lean ? wfpt::kPassLean : 0;
+  if (!fast) {  // deferred trials expected: the whole sequence at once
+    if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassAll | lp | wfpt::kPassRedo, d))
+      return rc;
+  } else {
+    if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassFast | lp, d)) return rc;
+    if (int rc = wait_result(c, c->mres)) return rc;
+    if (res_deferred(c->mres)) {
+      if (int rc = check_status_value(c->mres[2])) return rc;
+      if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev,
+                           wfpt::kPassDeferred | (lean ? wfpt::kPassRedo : 0), d))
+        return rc;
+    }
   }
-  d->no_defer = false;
-  if (int rc = check_status_value(c->mres[2])) return rc;
-  if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassDeferred, d)) return rc;
-  if (int rc = wait_result(c, c->mres)) return rc;
-  split_advance(d, eng, c->mres);
-  return decode_sum(c, c->mres, out);
+  return finish_sum(c, d, P, K, out, lean);
 }
 
 int upload(wfpt_ctx* c, const double* x, int64_t n) {
@@ -459,6 +502,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
+  if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -472,6 +516,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->prof, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->prof, 0, 16 * sizeof(int));
   if (e == hipSuccess)
@@ -509,6 +555,8 @@ void wfpt_close(wfpt_ctx* c) {
   c->nd_idx.release();
   c->nd_par.release();
   if (c->n_defer) (void)hipFree(c->n_defer);
+  if (c->tree_any) (void)hipFree(c->tree_any);
+  c->redo.release();
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -639,15 +687,10 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
   }
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  int rc = run_sum_fast(c, d, P, K, out);
+  const int rc = run_sum_fast(c, d, P, K, out);
   if (rc >= 0) return rc;
   if (int rc2 = run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassAll, d)) return rc2;
-  bool deferred = true;
-  if (int rc2 = wait_result(c, c->mres)) return rc2;
-  split_advance(d, engine_family(P, K), c->mres);
-  rc = decode_sum(c, c->mres, out, &deferred);
-  if (rc == WFPT_OK && c->fast_only) d->no_defer = !deferred;
-  return rc;
+  return finish_sum(c, d, P, K, out, false);
 }
 
 int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
@@ -873,7 +916,13 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   HIP_TRY(c->res.reserve(6));
-  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p, wfpt::kPassAll, d)) return rc;
+  // no host round trip before the exchange: the lean prediction runs the
+  // redo pass unconditionally (an empty one exits per wave on its flag)
+  const bool eng = engine_family(P, K);
+  const bool lean = eng && c->lean && d->no_tree && !c->count;
+  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p,
+                       wfpt::kPassAll | (lean ? wfpt::kPassLean | wfpt::kPassRedo : 0), d))
+    return rc;
   // {sum, zeros, encoded errors} of every rank summed: any zero trial or
   // failure anywhere reaches every rank (the error encoding keeps depth and
   // budget failures apart under the sum, wfpt_internal.h: kBudgetUnit)
@@ -883,8 +932,10 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   wfpt::launch_publish(c->res.p, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
-  split_advance(d, engine_family(P, K), c->mres);
-  return decode_sum(c, c->mres, out);
+  split_advance(d, eng && !lean, c->mres);
+  const int rc = decode_sum(c, c->mres, out);
+  if (rc == WFPT_OK && eng) d->no_tree = !res_tree(c->mres);
+  return rc;
 }
 
 int wfpt_profile_enable(wfpt_ctx* c, int flags) {

@@ -24,6 +24,12 @@ struct Work {
   int* rflag;         // [nslots] kFlagExact | kFlagFallback of the trial in slot
   int* prof;          // [16] refinement work counters (evaluation counting only)
   unsigned long long* phase;  // [8 * kPhaseWaves] per-wave engine timing (WFPT_PHASE_TIMING)
+  // Lean level-0 pass (kPassLean) and the engine's redo pass (kPassRedo): 1 =
+  // the chunk needs in-wave refinement, which the lean pass leaves to the
+  // engine (0 at rest: the redo pass clears what it handles). Null in a
+  // launch that is not the redo pass.
+  unsigned char* redo;        // [chunks]
+  int* tree_any;              // device word: some chunk of the call refined (0 at rest)
   int64_t nslots;
 };
 
@@ -64,22 +70,29 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 
 // out_kind: 0 = partial {sum, zeros}; 1 = per-trial density (logp => log);
 // 2 = per-trial log p. part: kPassFast (level-0 pass, or the whole fixed
-// Simpson kernel) | kPassDeferred (the deferred trials + fold). fast_done
-// (optional) is recorded right after the engine / trial kernel.
-constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3;
+// Simpson kernel) | kPassDeferred (the deferred trials + fold). Adaptive
+// families only: kPassLean makes the level-0 pass the lean kernel (level 0
+// without the in-wave refinement; a chunk that refines is flagged in W.redo
+// and counted as deferred), and kPassRedo runs the engine over the flagged
+// chunks (before the fold). fast_done (optional) is recorded right after the
+// level-0 / trial kernel.
+constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPassRedo = 8;
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,
                    const Split* split = nullptr);
-// out[0..3] = {sum of nb partials, #zero trials, encoded error flags, deferred
-// (any wl_n[0..nw) != 0; wl_n may be null)}, out[5] = *split_rd (the heavy
-// chunks the call recorded, or 0; then *split_rs = 0), then out[4] = seq (a
-// 64-bit word) once they are visible; resets *status to 0.
+// out[0..3] = {sum of nb partials, #zero trials, encoded error flags,
+// kResDeferred (any wl_n[0..nw) != 0; wl_n may be null) | kResTree (*tree_any;
+// then *tree_any = 0)}, out[5] = *split_rd (the heavy chunks the call
+// recorded, or 0; then *split_rs = 0), then out[4] = seq (a 64-bit word) once
+// they are visible; resets *status to 0.
+constexpr int kResDeferred = 1, kResTree = 2;
 void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
-                     const int* split_rd = nullptr, int* split_rs = nullptr);
-// res[0..2], res[5] (device) -> out[0..2], out[5] (mapped host), out[3] = 0,
-// then out[4] = seq.
+                     const int* split_rd = nullptr, int* split_rs = nullptr,
+                     int* tree_any = nullptr);
+// res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then
+// out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
 // two-pass fast path; d_idx / d_par hold up to n deferred trials, *n_defer

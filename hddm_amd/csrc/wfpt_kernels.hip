@@ -634,6 +634,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
   const int slot = split ? (int)(u / kSplit) : 0, sub = split ? (int)(u % kSplit) : 0;
   const int64_t c = split ? (int64_t)S.list[slot] : u - (int64_t)S.n * kSplit;
   if (!split && (c * 64 >= A.n || (S.n > 0 && S.pred[c]))) return;  // past the end / split
+  if (W.redo && !W.redo[c]) return;  // redo pass: only the chunks the lean pass flagged
   const int64_t i = split ? c * 64 + sub * kSplitTrials + lane : c * 64 + lane;
   const bool own = (split ? lane < kSplitTrials : true) && i < A.n;
   const double x0 = own ? A.x[i] : 0.0;
@@ -693,6 +694,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
   Tally ty;
   int nz0 = 0;
   if (rounds) {
+    if (lane == 0) *W.tree_any = 1;  // same-value plain stores: no atomic
     wave_sync();
     nz0 = cl.qn[1];
     pc.mark(1);
@@ -704,7 +706,10 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
     if (COUNT && lane == 0) tally_out(W, ty);
     return;
   }
-  if (lane == 0) record_heavy(S, c, nz0 > kHeavyZ);
+  if (lane == 0) {
+    record_heavy(S, c, nz0 > kHeavyZ);
+    if (W.redo) W.redo[c] = 0;
+  }
   bool defer = oc == kExact;
   int rf = kFlagExact;
   if (oc == kTree) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
@@ -720,6 +725,57 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
   }
 #endif
   if (COUNT && lane == 0) tally_out(W, ty);
+}
+
+// The engine's level 0 alone (kPassLean), for resident datasets whose last
+// call refined no chunk in-wave (the usual MCMC case at HDDM's knobs): no LDS,
+// no refinement code, so the register allocation and occupancy are those of
+// level 0 (FastWaves) instead of the engine's. Each lane runs eng_level0 on
+// the table's root z grid, i.e. the same operations on the same inputs as the
+// engine's level 0, and a chunk without refining trials leaves the bits the
+// engine would (chunk_out). A chunk with a refining trial writes nothing but
+// its redo flag and a nonzero deferred count; the engine's redo pass
+// (kPassRedo) then processes it from scratch, as a full engine call would.
+__device__ inline ZGrid zgrid_pick(const EngTables& tab, bool pos) {
+  const ZGrid& g0 = tab.G[0][kGridRoot];
+  const ZGrid& g1 = tab.G[1][kGridRoot];
+  ZGrid G;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    G.g[k] = pos ? g1.g[k] : g0.g[k];
+    G.A[k] = pos ? g1.A[k] : g0.A[k];
+  }
+  G.s0 = pos ? g1.s0 : g0.s0;
+  G.c0 = pos ? g1.c0 : g0.c0;
+  G.s4 = pos ? g1.s4 : g0.s4;
+  G.c4 = pos ? g1.c4 : g0.c4;
+  G.sd = pos ? g1.sd : g0.sd;
+  G.cd = pos ? g1.cd : g0.cd;
+  return G;
+}
+
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void lean_kernel(TrialArgs A, Work W, EngTables tab) {
+  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t c = i >> 6;
+  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
+  const bool own = i < A.n;
+  const double x0 = own ? A.x[i] : 0.0;
+  double p = 0.0, f0[5];
+  long long ne0 = 0;
+  unsigned pend0 = 0u;
+  int oc = kFinal;
+  if (own) oc = eng_level0<MODE>(x0, A.P, A.K, zgrid_pick(tab, x0 > 0), p, f0, ne0, pend0);
+  if (__ballot(oc == kTree) != 0ull) {
+    if (lane == 0) {
+      W.redo[c] = 1;
+      W.wl_n[c] = 1;  // finalize reports the call as deferred: the host runs the redo pass
+    }
+    return;
+  }
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
 }
 
 // Settles every deferred trial and folds it into its chunk: block g walks
@@ -812,7 +868,8 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
                                                         int64_t nb, const int* wl_n, int64_t nw,
                                                         int* status, double* out,
                                                         unsigned long long seq,
-                                                        const int* split_rd, int* split_rs) {
+                                                        const int* split_rd, int* split_rs,
+                                                        int* tree_any) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
   __shared__ int sd[16];
@@ -858,7 +915,12 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     out[0] = t;
     out[1] = (double)zz;
     out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
-    out[3] = (double)dd;
+    int res3 = dd ? kResDeferred : 0;
+    if (tree_any) {
+      if (*tree_any) res3 |= kResTree;
+      *tree_any = 0;
+    }
+    out[3] = (double)res3;
     // heavy chunks recorded for the next call (Split)
     out[5] = split_rd ? (double)*split_rd : 0.0;
     if (split_rs) *split_rs = 0;
@@ -878,7 +940,7 @@ __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* 
     out[0] = res[0];
     out[1] = res[1];
     out[2] = res[2];
-    out[3] = 0.0;
+    out[3] = res[3];
     out[5] = res[5];
     __threadfence_system();
     reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
@@ -1142,10 +1204,13 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
 
 template <int MODE, bool COUNT, int OUT>
 static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
-                     hipStream_t s, hipEvent_t fast_done) {
+                     bool lean, hipStream_t s, hipEvent_t fast_done) {
   if constexpr (MODE == kDirect) {
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W);
+  } else if (lean) {
+    hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
+                       0, s, A, W, T);
   } else {
     const int64_t units = (int64_t)S.n * kSplit + (A.n + 63) / 64;
     hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>),
@@ -1156,9 +1221,15 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
 }
 
 template <int MODE, bool COUNT, int OUT>
-static void run_deferred(const TrialArgs& A, const Work& W, hipStream_t s) {
-  // one wave per chunk up to WFPT_FOLD_GRID waves
+static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, bool redo,
+                         hipStream_t s) {
   const int64_t nw = (A.n + 63) / 64;
+  if constexpr (MODE != kDirect) {
+    if (redo)  // the engine over the chunks the lean pass flagged (one wave each)
+      hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>), dim3((nw + kEngWaves - 1) / kEngWaves),
+                         dim3(kEngBlock), 0, s, A, W, T, Split{});
+  }
+  // fold: one wave per chunk up to WFPT_FOLD_GRID waves
   const int64_t gf = std::min<int64_t>(WFPT_FOLD_GRID, nw);
   hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(64), 0, s, A, W, nw);
 }
@@ -1168,10 +1239,17 @@ static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, c
                         hipStream_t s, hipEvent_t fast_done) {
   EngTables T;
   if (mode >= kAdaptT && mode <= kAdaptTZ) eng_tables(A.P, T);
+  // W.redo is live only in the lean and redo passes (a full engine launch
+  // processes every chunk); the host never combines kPassRedo with a full
+  // engine level-0 pass
+  Work F = W;
+  F.redo = (part & (kPassLean | kPassRedo)) ? W.redo : nullptr;
 #define FAST_AND_DEFERRED(M_)                                               \
   do {                                                                      \
-    if (part & kPassFast) run_fast<M_, COUNT, OUT>(A, W, T, S, s, fast_done); \
-    if (part & kPassDeferred) run_deferred<M_, COUNT, OUT>(A, W, s);        \
+    if (part & kPassFast)                                                   \
+      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, s, fast_done); \
+    if (part & kPassDeferred)                                               \
+      run_deferred<M_, COUNT, OUT>(A, F, T, (part & kPassRedo) != 0, s);    \
   } while (0)
   switch (mode) {
     case kDirect: FAST_AND_DEFERRED(kDirect); break;
@@ -1227,9 +1305,9 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
-                     const int* split_rd, int* split_rs) {
+                     const int* split_rd, int* split_rs, int* tree_any) {
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, wl_n, nw, status,
-                     out, seq, split_rd, split_rs);
+                     out, seq, split_rd, split_rs, tree_any);
 }
 
 template <int MODE, bool COUNT>
