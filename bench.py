@@ -21,7 +21,6 @@ With --gpus N > 1 and no WORLD_SIZE in the environment this process launches
 exits with the launcher's code.
 """
 import argparse
-import hashlib
 import json
 import os
 import subprocess
@@ -111,10 +110,14 @@ def cpu_baseline(x, budget_s):
                       f"{v1:.3e} trials/s)"}
 
 
-def pmc_summary(lib_path, n_trials):
+def pmc_summary(lib_path):
     """Executed-work figures of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/traffic.json, written by tools/summarize_profile.py),
-    used only if it was measured on this very library build and size."""
+    used only if it was measured on a library built from the same sources and
+    flags as the one loaded (hddm_amd.build.source_digest, recorded at build
+    time next to the .so). Per-trial figures: the C3 and C5 datasets are
+    samples of the same model."""
+    from hddm_amd import build as hb
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None
@@ -123,9 +126,8 @@ def pmc_summary(lib_path, n_trials):
             t = json.load(fh)
     except Exception:
         return None
-    with open(lib_path, "rb") as fh:
-        digest = hashlib.sha1(fh.read()).hexdigest()
-    t["matches_build"] = (t.get("lib_sha1") == digest and int(t.get("n_trials", -1)) == n_trials)
+    digest = hb.built_digest(lib_path)
+    t["matches_build"] = digest is not None and t.get("src_sha1") == digest
     return t
 
 
@@ -228,10 +230,10 @@ def main():
     glob = n * world
     value = glob * a.steps / el
     k_avg_s = (k_ms / 1e3) / max(launches, 1)
-    pmc = pmc_summary(_lib.LIB_PATH, n)
+    pmc = pmc_summary(_lib.LIB_PATH)
     roof = {"bound": "valu-fp64", "peak": PEAK_LANE_OPS / 1e12, "unit": "T fp64-lane-ops/s",
             "achieved": None, "frac": None, "traffic": None,
-            "kernel": "wfpt::fast_kernel<3, false, 0> (level-0 pass)",
+            "kernel": "wfpt::lean_kernel<3, false, 0> (level-0 pass)",
             "kernel_ms_avg": k_avg_s * 1e3, "kernel_launches": launches}
     if pmc and pmc.get("matches_build"):
         # executed fp64 VALU lane-ops per trial of this kernel (rocprofv3
@@ -239,8 +241,10 @@ def main():
         # over its live per-launch time
         w = float(pmc["fp64_lane_ops_per_trial"])
         achieved = n * w / k_avg_s / 1e12
+        traffic = pmc.get("hbm_bytes_per_trial")
         roof.update(achieved=achieved, frac=achieved / (PEAK_LANE_OPS / 1e12),
-                    traffic=pmc.get("hbm_bytes_per_launch"), fp64_lane_ops_per_trial=w,
+                    traffic=traffic * n if traffic is not None else None,
+                    fp64_lane_ops_per_trial=w,
                     valu_issue_utilisation=pmc.get("valu_issue_utilisation"),
                     algorithmic_bytes=8.0 * n, pmc_source=pmc.get("source"))
     else:

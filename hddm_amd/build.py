@@ -24,6 +24,29 @@ CFLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fPIC",
           f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-result"]
 
 
+def source_digest(defines=()):
+    """sha1 over the compiler flags and every source the library is built from:
+    identifies a build independently of the binary's bytes (profiles measured
+    on one build are matched to the library by it)."""
+    import hashlib
+    h = hashlib.sha1(" ".join(CFLAGS + list(defines)).encode())
+    for f in DEPS:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(fh.read())
+    with open(os.path.join(ROOT, "include", "wfpt_amd.h"), "rb") as fh:
+        h.update(fh.read())
+    return h.hexdigest()
+
+
+def built_digest(lib=LIB):
+    """The source digest recorded next to a built library (None if absent)."""
+    try:
+        with open(lib + ".src") as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
 def _stale(target, deps):
     if not os.path.exists(target):
         return True
@@ -39,6 +62,9 @@ def build(force=False, verbose=False, defines=(), out=None):
     lib = out or LIB
     deps = [os.path.join(CSRC, f) for f in DEPS] + [os.path.join(ROOT, "include", "wfpt_amd.h")]
     if not force and not _stale(lib, deps):
+        if built_digest(lib) is None:  # built before digests were recorded
+            with open(lib + ".src", "w") as fh:
+                fh.write(source_digest(defines) + "\n")
         return lib
     objs = []
     tag = os.path.splitext(os.path.basename(lib))[0]
@@ -58,6 +84,8 @@ def build(force=False, verbose=False, defines=(), out=None):
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(tmp, lib)
+    with open(lib + ".src", "w") as fh:
+        fh.write(source_digest(defines) + "\n")
     for o in objs:
         os.remove(o)
     return lib

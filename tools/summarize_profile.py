@@ -8,12 +8,12 @@ the bytes of a wide coalesced stream on gfx950, so it is doubled; WRITE_SIZE
 
     python tools/summarize_profile.py r02 [--kernel 'void wfpt::fast_kernel<3, false, 0>']
 
-traffic.json carries the sha1 of hddm_amd/lib/libwfpt_amd.so (the build that
-was shipped to the GPU box and profiled): bench.py uses the executed-work
-figures only while that build is the one it loads.
+traffic.json carries the source digest of hddm_amd/lib/libwfpt_amd.so (flags +
+sources of the build that was shipped to the GPU box and profiled,
+hddm_amd.build.source_digest): bench.py uses the executed-work figures only
+while the library it loads was built from those sources.
 """
 import argparse
-import hashlib
 import collections
 import csv
 import json
@@ -39,7 +39,7 @@ def per_launch(path, kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--kernel", default="void wfpt::fast_kernel<3, false, 0>")
+    ap.add_argument("--kernel", default="void wfpt::lean_kernel<3, false, 0>")
     ap.add_argument("--trials", type=int, default=1_000_000)
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "profiles", a.tag)
@@ -79,15 +79,17 @@ def main():
         json.dump(summary, fh, indent=1)
     shutil.copy(os.path.join(PROF, "trace", "trace_kernel_stats.csv"),
                 os.path.join(out_dir, "kernel_stats.csv"))
-    lib = os.path.join(ROOT, "hddm_amd", "lib", "libwfpt_amd.so")
-    with open(lib, "rb") as fh:
-        sha = hashlib.sha1(fh.read()).hexdigest()
-    summary["lib_sha1"] = sha
+    import sys
+    sys.path.insert(0, ROOT)
+    from hddm_amd import build as hb
+    sha = hb.built_digest()
+    summary["src_sha1"] = sha
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
     with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as fh:
-        json.dump({"lib_sha1": sha, "source": f"profiles/{a.tag}/pmc_summary.json", "kernel": a.kernel,
+        json.dump({"src_sha1": sha, "source": f"profiles/{a.tag}/pmc_summary.json", "kernel": a.kernel,
                    "n_trials": a.trials, "hbm_bytes_per_launch": fetch_b + write_b,
+                   "hbm_bytes_per_trial": (fetch_b + write_b) / a.trials,
                    "valu_issue_utilisation": summary["valu_issue_utilisation"],
                    "fp64_lane_ops_per_trial": summary["fp64_lane_ops_per_trial"],
                    "valu_lane_ops_per_trial": summary["valu_lane_ops_per_trial"]}, fh, indent=1)
