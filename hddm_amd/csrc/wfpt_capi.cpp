@@ -335,8 +335,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
                       c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
                       prof ? c->ev1 : nullptr, &S);
   HIP_TRY(hipGetLastError());
-  const int64_t nw = (n + 63) / 64;
-  wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? W.wl_n : nullptr, adaptive ? nw : 0,
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? 1 : 0,
                         c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
                         eng ? d->hcount + d->parity : nullptr, c->tree_any);
   HIP_TRY(hipGetLastError());
@@ -829,7 +828,7 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   wfpt::launch_multi(c->x.p, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
                      c->status, c->stream);
   HIP_TRY(hipGetLastError());
-  wfpt::launch_finalize(c->part.p, c->zero.p, nb, nullptr, 0, c->status, c->mres_dev, ++c->seq,
+  wfpt::launch_finalize(c->part.p, c->zero.p, nb, 0, c->status, c->mres_dev, ++c->seq,
                         c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;

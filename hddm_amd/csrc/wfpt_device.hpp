@@ -1360,6 +1360,18 @@ __host__ __device__ inline void eng_tables(const Params& P, EngTables& T) {
   }
 }
 
+// The root z grids of both boundaries alone (the lean level-0 pass): the
+// same zgrid_of calls as eng_tables' G[flip][kGridRoot], so bit-identical.
+struct RootGrids {
+  ZGrid G[2];
+};
+__host__ __device__ inline void root_grids(const Params& P, RootGrids& R) {
+  for (int flip = 0; flip < 2; ++flip) {
+    const double zf = flip ? 1. - P.z : P.z, vf = flip ? -P.v : P.v;
+    R.G[flip] = zgrid_of(zf - P.sz / 2., zf + P.sz / 2., kGridRoot, vf, P.sv, P.a);
+  }
+}
+
 // P(hit upper boundary), pdf.pxi:67-72
 __device__ inline double prob_ub(double v, double a, double z) {
   if (v == 0) return z;

@@ -82,12 +82,12 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,
                    const Split* split = nullptr);
 // out[0..3] = {sum of nb partials, #zero trials, encoded error flags,
-// kResDeferred (any wl_n[0..nw) != 0; wl_n may be null) | kResTree (*tree_any;
-// then *tree_any = 0)}, out[5] = *split_rd (the heavy chunks the call
+// kResDeferred (defer_bits: some chunk's zero word carries kZeroDefer) |
+// kResTree (*tree_any; then *tree_any = 0)}, out[5] = *split_rd (the heavy chunks the call
 // recorded, or 0; then *split_rs = 0), then out[4] = seq (a 64-bit word) once
 // they are visible; resets *status to 0.
 constexpr int kResDeferred = 1, kResTree = 2;
-void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
+void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
                      const int* split_rd = nullptr, int* split_rs = nullptr,
                      int* tree_any = nullptr);

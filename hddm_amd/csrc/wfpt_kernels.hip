@@ -58,6 +58,9 @@ struct FastWaves {
 #endif
 
 enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
+// OUT_SUM per-chunk zero-count word: zero-density trials | kZeroDefer if the
+// chunk's level-0 pass deferred trials (or left the chunk to the redo pass)
+constexpr int kZeroDefer = 1 << 16;
 
 __device__ inline double wave_sum(double v) {
 #pragma unroll
@@ -127,7 +130,9 @@ __device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp,
 // kTreeDepth) takes slot c * 64 + k of its chunk c (k = its rank among the
 // chunk's deferred trials): no atomic, and fold_kernel finds a chunk's
 // deferred trials on its first lanes.
-__device__ inline void defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag) {
+// Returns whether the chunk deferred any trial (its zero-count word then
+// carries kZeroDefer, which finalize reports).
+__device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag) {
   const unsigned long long b = __ballot(defer);
   if (defer) {
     const int64_t slot = c * 64 + __popcll(b & lanemask_lt(lane));
@@ -135,6 +140,7 @@ __device__ inline void defer_slots(const Work& W, int64_t c, int lane, bool defe
     W.rflag[slot] = rflag;
   }
   if (lane == 0) W.wl_n[c] = __popcll(b);
+  return b != 0ull;
 }
 
 // Direct family (sz = st = 0): one pdf_sv per trial, one chunk of 64 trials
@@ -154,13 +160,13 @@ void fast_kernel(TrialArgs A, Work W) {
   int zero = 0;
   if (i < A.n && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
   if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
-  defer_slots(W, c, lane, oc != kFinal, kFlagExact);
+  const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
   if (OUT == OUT_SUM) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
     if (lane == 0) {
       A.out[c] = lp;
-      A.zeros[c] = zs;
+      A.zeros[c] = zs | (anyd ? kZeroDefer : 0);
     }
   }
   if (COUNT) {
@@ -521,13 +527,13 @@ __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, i
   double lp = 0.0;
   int zero = 0;
   if (i < A.n && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
-  defer_slots(W, c, lane, defer, rf);
+  const bool anyd = defer_slots(W, c, lane, defer, rf);
   if (OUT == OUT_SUM) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
     if (lane == 0) {
       A.out[c] = lp;
-      A.zeros[c] = zs;
+      A.zeros[c] = zs | (anyd ? kZeroDefer : 0);
     }
   }
   if (COUNT) {
@@ -598,13 +604,13 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const double lpc = S.lp[slot * 64 + lane];
   const int m = S.meta[slot * 64 + lane];
-  defer_slots(W, c, lane, (m >> 1) & 1, m >> 2);
+  const bool anyd = defer_slots(W, c, lane, (m >> 1) & 1, m >> 2);
   if (OUT == OUT_SUM) {
     const double sum = wave_sum(lpc);
     const int zs = __popcll(__ballot((m & 1) != 0));
     if (lane == 0) {
       A.out[c] = sum;
-      A.zeros[c] = zs;
+      A.zeros[c] = zs | (anyd ? kZeroDefer : 0);
     }
   }
   if (lane == 0) {
@@ -736,9 +742,9 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
 // engine would (chunk_out). A chunk with a refining trial writes nothing but
 // its redo flag and a nonzero deferred count; the engine's redo pass
 // (kPassRedo) then processes it from scratch, as a full engine call would.
-__device__ inline ZGrid zgrid_pick(const EngTables& tab, bool pos) {
-  const ZGrid& g0 = tab.G[0][kGridRoot];
-  const ZGrid& g1 = tab.G[1][kGridRoot];
+__device__ inline ZGrid zgrid_pick(const RootGrids& R, bool pos) {
+  const ZGrid& g0 = R.G[0];
+  const ZGrid& g1 = R.G[1];
   ZGrid G;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
@@ -756,7 +762,7 @@ __device__ inline ZGrid zgrid_pick(const EngTables& tab, bool pos) {
 
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void lean_kernel(TrialArgs A, Work W, EngTables tab) {
+void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
@@ -767,11 +773,12 @@ void lean_kernel(TrialArgs A, Work W, EngTables tab) {
   long long ne0 = 0;
   unsigned pend0 = 0u;
   int oc = kFinal;
-  if (own) oc = eng_level0<MODE>(x0, A.P, A.K, zgrid_pick(tab, x0 > 0), p, f0, ne0, pend0);
+  if (own) oc = eng_level0<MODE>(x0, A.P, A.K, zgrid_pick(R, x0 > 0), p, f0, ne0, pend0);
   if (__ballot(oc == kTree) != 0ull) {
     if (lane == 0) {
       W.redo[c] = 1;
-      W.wl_n[c] = 1;  // finalize reports the call as deferred: the host runs the redo pass
+      // finalize reports the call as deferred: the host runs the redo pass
+      if (OUT == OUT_SUM) A.zeros[c] = kZeroDefer;
     }
     return;
   }
@@ -859,13 +866,15 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
 
 // out[0] = sum of nb partials, out[1] = number of zero trials, out[2] = error
 // flags encoded as counts that survive a sum over ranks (depth + 2^20 budget),
-// out[3] = 1 if the level-0 pass deferred trials (wl_n non-null: any chunk
-// count), then the 64-bit completion word out[4] once they are visible. `out`
-// may be mapped pinned host memory. Resets the device status word. Fixed
-// summation order for a given nb (4 accumulators per thread keep 4 loads in
-// flight).
+// out[3] = kResDeferred if some chunk's word carries kZeroDefer (defer_bits:
+// per-chunk partials of the adaptive / direct families) | kResTree, then the
+// 64-bit completion word out[4] once they are visible. `out` may be mapped
+// pinned host memory. Resets the device status word. Fixed summation order
+// for a given nb: thread k owns partials k + 1024 j, loaded kFinLoads at a
+// time (all in flight together) and summed in j order; then a fixed tree.
+constexpr int kFinLoads = 16;
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
-                                                        int64_t nb, const int* wl_n, int64_t nw,
+                                                        int64_t nb, int defer_bits,
                                                         int* status, double* out,
                                                         unsigned long long seq,
                                                         const int* split_rd, int* split_rs,
@@ -873,24 +882,26 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
   __shared__ double ss[16];
   __shared__ long long sz[16];
   __shared__ int sd[16];
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  double s = 0.0;
   long long z = 0;
-  int64_t b = threadIdx.x;
-  for (; b + 3 * 1024 < nb; b += 4 * 1024) {
-    s0 += part[b];
-    s1 += part[b + 1024];
-    s2 += part[b + 2048];
-    s3 += part[b + 3072];
-    z += (long long)zeros[b] + zeros[b + 1024] + zeros[b + 2048] + zeros[b + 3072];
-  }
-  for (; b < nb; b += 1024) {
-    s0 += part[b];
-    z += zeros[b];
-  }
   int def = 0;
-  if (wl_n)
-    for (int64_t c = threadIdx.x; c < nw; c += 1024) def |= wl_n[c];
-  double s = (s0 + s1) + (s2 + s3);
+  for (int64_t b0 = threadIdx.x; b0 < nb; b0 += kFinLoads * 1024) {
+    double v[kFinLoads];
+    int w[kFinLoads];
+#pragma unroll
+    for (int j = 0; j < kFinLoads; ++j) {
+      const int64_t b = b0 + (int64_t)j * 1024;
+      v[j] = b < nb ? part[b] : 0.0;
+      w[j] = b < nb ? zeros[b] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kFinLoads; ++j) {
+      s += v[j];
+      z += w[j] & (kZeroDefer - 1);
+      def |= w[j];
+    }
+  }
+  def = defer_bits ? (def & kZeroDefer) : 0;
   s = wave_sum(s);
   z = wave_sum_ll(z);
   const bool anyd = __ballot(def != 0) != 0ull;
@@ -1209,8 +1220,10 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W);
   } else if (lean) {
+    RootGrids R;
+    root_grids(A.P, R);
     hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
-                       0, s, A, W, T);
+                       0, s, A, W, R);
   } else {
     const int64_t units = (int64_t)S.n * kSplit + (A.n + 63) / 64;
     hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>),
@@ -1237,8 +1250,10 @@ static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, 
 template <bool COUNT, int OUT>
 static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, const Split& S,
                         hipStream_t s, hipEvent_t fast_done) {
+  // the engine's tables (the lean pass alone needs only its root grids)
   EngTables T;
-  if (mode >= kAdaptT && mode <= kAdaptTZ) eng_tables(A.P, T);
+  const bool engine = ((part & kPassFast) && !(part & kPassLean)) || (part & kPassRedo);
+  if (mode >= kAdaptT && mode <= kAdaptTZ && engine) eng_tables(A.P, T);
   // W.redo is live only in the lean and redo passes (a full engine launch
   // processes every chunk); the host never combines kPassRedo with a full
   // engine level-0 pass
@@ -1303,11 +1318,11 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
   }
 }
 
-void launch_finalize(const double* part, const int* zeros, int64_t nb, const int* wl_n, int64_t nw,
+void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
                      const int* split_rd, int* split_rs, int* tree_any) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, wl_n, nw, status,
-                     out, seq, split_rd, split_rs, tree_any);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, defer_bits,
+                     status, out, seq, split_rd, split_rs, tree_any);
 }
 
 template <int MODE, bool COUNT>

@@ -176,10 +176,19 @@ class Dataset:
     def __len__(self):
         return self.n
 
+    def _knobs(self, err, n_st, n_sz, use_adaptive, simps_err, w_outlier):
+        """The knobs struct, rebuilt only when the knobs change (they are fixed
+        across an MCMC run; per-call Python work sits in front of the kernel)."""
+        key = (err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        kc = getattr(self, "_kc", None)
+        if kc is None or kc[0] != key:
+            kc = self._kc = (key, _lib.make_knobs(*key))
+        return kc[1]
+
     def wiener_like(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10, use_adaptive=1,
                     simps_err=1e-8, p_outlier=0, w_outlier=0.1):
         P = _lib.make_params(v, sv, a, z, sz, t, st, p_outlier)
-        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = ctypes.c_double()
         _lib.check(_lib.wfpt_wiener_like(self.ctx.handle, self.handle, ctypes.byref(P),
                                          ctypes.byref(K), ctypes.byref(out)))
