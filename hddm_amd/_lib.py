@@ -65,6 +65,10 @@ wfpt_open = _sig("wfpt_open", _I, [_I, ctypes.POINTER(_VP)])
 wfpt_close = _sig("wfpt_close", None, [_VP])
 wfpt_dataset_create = _sig("wfpt_dataset_create", _I,
                            [_VP, _PD, _I64, ctypes.POINTER(_I32), _I32, ctypes.POINTER(_VP)])
+wfpt_dataset_create_ex = _sig("wfpt_dataset_create_ex", _I,
+                              [_VP, _PD, _I64, ctypes.POINTER(_I32), _I32, _I,
+                               ctypes.POINTER(_VP)])
+WFPT_DS_INPUT_ORDER = 1
 wfpt_dataset_destroy = _sig("wfpt_dataset_destroy", None, [_VP])
 wfpt_dataset_size = _sig("wfpt_dataset_size", _I64, [_VP])
 wfpt_shard_range = _sig("wfpt_shard_range", None,
@@ -76,6 +80,8 @@ wfpt_pdf_array = _sig("wfpt_pdf_array", _I, [_VP, _PD, _I64, _PP, _PK, _I, _PD])
 wfpt_full_pdf = _sig("wfpt_full_pdf", _I, [_VP, _D, _PP, _PK, _PD])
 wfpt_wiener_like_multi = _sig("wfpt_wiener_like_multi", _I,
                               [_VP, _PD, _I64, ctypes.POINTER(_PD), _PD, _PK, _D, _PD])
+wfpt_wiener_like_multi_resident = _sig("wfpt_wiener_like_multi_resident", _I,
+                                       [_VP, _VP, ctypes.POINTER(_PD), _PD, _PK, _D, _PD])
 wfpt_dmat_cdf_array = _sig("wfpt_dmat_cdf_array", _I, [_VP, _PD, _I64, _PP, _D, _PD])
 wfpt_comm_unique_id = _sig("wfpt_comm_unique_id", _I, [ctypes.c_char_p])
 wfpt_comm_init = _sig("wfpt_comm_init", _I, [_VP, _I, _I, ctypes.c_char_p])
@@ -97,7 +103,8 @@ EXPORTED = [
     "wfpt_wiener_like_host", "wfpt_wiener_like_nodes", "wfpt_pdf_array", "wfpt_full_pdf",
     "wfpt_wiener_like_multi", "wfpt_dmat_cdf_array", "wfpt_comm_unique_id", "wfpt_comm_init",
     "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
-    "wfpt_decode_result", "wfpt_profile_lists", "wfpt_debug_waves",
+    "wfpt_decode_result", "wfpt_profile_lists", "wfpt_debug_waves", "wfpt_dataset_create_ex",
+    "wfpt_wiener_like_multi_resident",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)

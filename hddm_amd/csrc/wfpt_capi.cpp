@@ -154,6 +154,7 @@ struct wfpt_ds {
   // the last call on this dataset refined no chunk in-wave: the next one's
   // level-0 pass is the lean kernel (kPassLean)
   mutable bool no_tree = false;
+  bool input_order = false;  // WFPT_DS_INPUT_ORDER: trials kept in the caller's order
   // heavy-chunk record (wfpt_internal.h: Split), double-buffered by call
   // parity: the engine writes [1 - parity] while it reads [parity]
   int64_t nw = 0;
@@ -579,14 +580,21 @@ void wfpt_shard_range(int64_t n, int nranks, int rank, int64_t* lo, int64_t* hi)
 
 int wfpt_dataset_create(wfpt_ctx* c, const double* rt, int64_t n, const int32_t* node_id,
                         int32_t n_nodes, wfpt_ds** out) {
+  return wfpt_dataset_create_ex(c, rt, n, node_id, n_nodes, 0, out);
+}
+
+int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32_t* node_id,
+                           int32_t n_nodes, int flags, wfpt_ds** out) {
   if (!c || !out || (n > 0 && !rt) || n < 0) return fail(WFPT_ERR_ARG, "bad dataset arguments");
+  if (flags & ~WFPT_DS_INPUT_ORDER) return fail(WFPT_ERR_ARG, "unknown dataset flags");
   if (node_id && n_nodes <= 0) return fail(WFPT_ERR_ARG, "node ids need n_nodes > 0");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   // host-side layout: group by node, order by |rt| inside a node so that each
   // wavefront sees one series branch / similar quadrature depth.
-  const bool keep_order = std::getenv("WFPT_DATASET_ORDER") &&
-                          std::strcmp(std::getenv("WFPT_DATASET_ORDER"), "input") == 0;
+  const bool keep_order = (flags & WFPT_DS_INPUT_ORDER) ||
+                          (std::getenv("WFPT_DATASET_ORDER") &&
+                           std::strcmp(std::getenv("WFPT_DATASET_ORDER"), "input") == 0);
   std::vector<int64_t> idx(n);
   for (int64_t i = 0; i < n; ++i) idx[i] = i;
   std::vector<int64_t> off;
@@ -617,6 +625,7 @@ int wfpt_dataset_create(wfpt_ctx* c, const double* rt, int64_t n, const int32_t*
   auto* d = new wfpt_ds();
   d->ctx = c;
   d->n = n;
+  d->input_order = (flags & WFPT_DS_INPUT_ORDER) != 0;
   d->n_nodes = node_id ? n_nodes : 0;
   hipError_t e = hipMalloc((void**)&d->x, std::max<int64_t>(n, 1) * sizeof(double));
   if (e == hipSuccess && n > 0)
@@ -792,15 +801,15 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   return WFPT_OK;
 }
 
-int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
-                           const double* const arrays[7], const double scalars[7],
-                           const wfpt_knobs* k, double p_outlier, double* out) {
-  if (!c || (!x && n > 0) || !arrays || !scalars || !k || !out || n < 0)
-    return fail(WFPT_ERR_ARG, "bad arguments");
-  const wfpt::Knobs K = to_knobs(k);
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
-  if (int rc = upload(c, x, n)) return rc;
+}  // extern "C"
+
+namespace {
+// wiener_like_multi over device x[n]: the per-trial parameter arrays go up for
+// this call; a uniform adaptive / direct family (sz and st scalar) takes the
+// level-0 pass + deferred records (launch_multi_fast), anything else the
+// generic per-trial kernel.
+int run_multi(wfpt_ctx* c, const double* dx, int64_t n, const double* const arrays[7],
+              const double scalars[7], const wfpt::Knobs& K, double p_outlier, double* out) {
   int na = 0;
   for (int j = 0; j < 7; ++j) na += arrays[j] != nullptr;
   HIP_TRY(c->marr.reserve(std::max<int64_t>((int64_t)na * n, 1)));
@@ -825,16 +834,62 @@ int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
   const int64_t nb = wfpt::blocks_for(n);
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
-  wfpt::launch_multi(c->x.p, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
-                     c->status, c->stream);
+  const int mode = (arrays[4] || arrays[6]) ? -1 : wfpt::select_mode(scalars[4], scalars[6],
+                                                                     K.use_adaptive);
+  if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  if (mode >= 0 && mode <= wfpt::kAdaptTZ && n > 0) {
+    HIP_TRY(c->lp.reserve(n));
+    HIP_TRY(c->nd_idx.reserve(n));
+    HIP_TRY(c->nd_par.reserve(n));
+    HIP_TRY(hipMemsetAsync(c->n_defer, 0, sizeof(int), c->stream));
+    wfpt::launch_multi_fast(mode, dx, n, c->mptr.p, c->mscal.p, K, p_outlier, c->lp.p,
+                            c->nd_idx.p, c->nd_par.p, c->n_defer, c->part.p, c->zero.p,
+                            c->count ? c->evals : nullptr, c->status, c->stream);
+  } else {
+    wfpt::launch_multi(dx, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
+                       c->status, c->stream);
+  }
   HIP_TRY(hipGetLastError());
+  if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, 0, c->status, c->mres_dev, ++c->seq,
                         c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
   if (int rc = check_status_value(c->mres[2])) return rc;
+  if (int rc = finish_profile(c)) return rc;
   *out = c->mres[0];
   return WFPT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
+                           const double* const arrays[7], const double scalars[7],
+                           const wfpt_knobs* k, double p_outlier, double* out) {
+  if (!c || (!x && n > 0) || !arrays || !scalars || !k || !out || n < 0)
+    return fail(WFPT_ERR_ARG, "bad arguments");
+  const wfpt::Knobs K = to_knobs(k);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if (int rc = upload(c, x, n)) return rc;
+  return run_multi(c, c->x.p, n, arrays, scalars, K, p_outlier, out);
+}
+
+int wfpt_wiener_like_multi_resident(wfpt_ctx* c, const wfpt_ds* d, const double* const arrays[7],
+                                    const double scalars[7], const wfpt_knobs* k,
+                                    double p_outlier, double* out) {
+  if (!c || !d || !arrays || !scalars || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  if (!d->input_order || d->node)
+    return fail(WFPT_ERR_ARG,
+                "wiener_like_multi on a dataset needs one created with WFPT_DS_INPUT_ORDER "
+                "and no node ids (per-trial arrays follow the caller's trial order)");
+  const wfpt::Knobs K = to_knobs(k);
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  return run_multi(c, d->x, d->n, arrays, scalars, K, p_outlier, out);
 }
 
 int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,

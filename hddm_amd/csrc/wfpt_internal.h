@@ -105,6 +105,14 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
 // the sums, [n_nodes] encoded error flags, [n_nodes + 1] the completion word.
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s);
+// wiener_like_multi with a uniform adaptive / direct family (mode): level-0
+// pass + deferred trials (d_idx / d_par hold up to n records, *n_defer must
+// be 0 on the stream) into lp[n], then per-block sums into part / zeros
+// (blocks_for(n) of them) for launch_finalize.
+void launch_multi_fast(int mode, const double* x, int64_t n, const double* const* arr,
+                       const double* scal, const Knobs& K, double p_outlier, double* lp,
+                       int64_t* d_idx, Params* d_par, int* n_defer, double* part, int* zeros,
+                       unsigned long long* evals, int* status, hipStream_t s);
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
                   const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
                   hipStream_t s);

@@ -1114,7 +1114,9 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   }
 }
 
-template <int MODE, int STK, bool COUNT>
+// MULTI: wiener_like_multi's trial term (wfpt.pyx:266-272: the mixture with
+// the call's p_outlier and a plain log, no range check) instead of a node's.
+template <int MODE, int STK, bool COUNT, bool MULTI = false>
 __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(
     const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
     const int* n_defer, unsigned long long* evals, int* status) {
@@ -1132,7 +1134,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(
     flags |= f1 & kFlagErrors;
     p = settle(p, x[i], Q, K, false, n1, flags);
     ne += n1;
-    lp[i] = node_logp(p, Q, K);
+    lp[i] = MULTI ? log(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier)) : node_logp(p, Q, K);
   }
   if (flags & kFlagErrors) atomicOr(status, flags & kFlagErrors);
   if (COUNT) {
@@ -1195,6 +1197,78 @@ int stack_kind(const Knobs& K) {
 }
 
 int64_t blocks_for(int64_t n) { return (n + kBlock - 1) / kBlock; }
+
+// wiener_like_multi's level-0 pass when the integration family is uniform
+// (sz and st are scalars, adaptive): one trial per lane with its own
+// parameters (per-trial arrays, or the scalars), the same fast_level0 as the
+// per-node path; trials whose root test refines (or hinge on rounding) go to
+// node_slow_kernel<..., MULTI> as (index, parameter row) records. |x| = 999
+// trials are scored by prob_ub (wfpt.pyx:267-271). lp[i] = the trial's term.
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void multi_fast_kernel(const double* x, int64_t n, const double* const* arr, const double* scal,
+                       Knobs K, double p_outlier, double* lp, int64_t* d_idx, Params* d_par,
+                       int* n_defer, unsigned long long* evals) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  long long ne = 0;
+  bool defer = false;
+  Params Q;
+  if (i < n) {
+    double q[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) q[j] = arr[j] ? arr[j][i] : scal[j];
+    Q.v = q[0];
+    Q.sv = q[1];
+    Q.a = q[2];
+    Q.z = q[3];
+    Q.sz = q[4];
+    Q.t = q[5];
+    Q.st = q[6];
+    Q.p_outlier = p_outlier;
+    const double xi = x[i];
+    if (fabs(xi) != 999.) {
+      double p, f[5];
+      int flags = 0;
+      unsigned pend;
+      const int oc = fast_level0<MODE>(xi, Q, K, p, f, ne, flags, pend);
+      if (oc == kFinal) lp[i] = log(p * (1 - p_outlier) + (K.w_outlier * p_outlier));
+      else defer = true;
+    } else {
+      const double pu = prob_ub(Q.v, Q.a, Q.z);
+      lp[i] = log(xi == 999. ? pu : 1 - pu);
+    }
+  }
+  const unsigned long long b = __ballot(defer);
+  if (b) {
+    int base = 0;
+    if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
+    base = __shfl(base, 0, 64);
+    if (defer) {
+      const int k = base + __popcll(b & lanemask_lt(lane));
+      d_idx[k] = i;
+      d_par[k] = Q;
+    }
+  }
+  if (COUNT) {
+    ne = wave_sum_ll(defer ? 0 : ne);
+    if (lane == 0) atomicAdd(evals, (unsigned long long)ne);
+  }
+}
+
+// Fixed-order per-block sums of per-trial terms (finalize adds the blocks).
+__global__ __launch_bounds__(kBlock) void lp_sum_kernel(const double* lp, int64_t n, double* part,
+                                                        int* zeros) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  double s = i < n ? lp[i] : 0.0;
+  int zero = 0;
+  long long ne = 0;
+  block_reduce<false>(s, zero, ne);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s;
+    zeros[blockIdx.x] = 0;
+  }
+}
 
 static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const Knobs& K,
                             double* out, int* zeros, unsigned long long* evals, int* status,
@@ -1398,6 +1472,51 @@ void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, d
                      n_nodes, res);
   hipLaunchKernelGGL(publish_nodes_kernel, dim3(1), dim3(256), 0, s, res, n_nodes, status, out,
                      seq);
+}
+
+template <int MODE, bool COUNT>
+static void launch_multi_two_pass(const double* x, int64_t n, const double* const* arr,
+                                  const double* scal, const Knobs& K, double p_outlier, double* lp,
+                                  int64_t* d_idx, Params* d_par, int* n_defer,
+                                  unsigned long long* evals, int* status, hipStream_t s) {
+  hipLaunchKernelGGL((multi_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
+                     n, arr, scal, K, p_outlier, lp, d_idx, d_par, n_defer, evals);
+  const int64_t nl = (n + 63) / 64;
+  const int64_t g = nl < 2048 ? nl : 2048;
+  const int stk = stack_kind(K);
+  if (stk == 0)
+    hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
+                       d_idx, d_par, n_defer, evals, status);
+  else if (stk == 1)
+    hipLaunchKernelGGL((node_slow_kernel<MODE, 1, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
+                       d_idx, d_par, n_defer, evals, status);
+  else
+    hipLaunchKernelGGL((node_slow_kernel<MODE, 2, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
+                       d_idx, d_par, n_defer, evals, status);
+}
+
+void launch_multi_fast(int mode, const double* x, int64_t n, const double* const* arr,
+                       const double* scal, const Knobs& K, double p_outlier, double* lp,
+                       int64_t* d_idx, Params* d_par, int* n_defer, double* part, int* zeros,
+                       unsigned long long* evals, int* status, hipStream_t s) {
+#define MULTI_TWO_PASS(M_, C_)                                                                  \
+  launch_multi_two_pass<M_, C_>(x, n, arr, scal, K, p_outlier, lp, d_idx, d_par, n_defer, evals, \
+                                status, s)
+#define MULTI_MODES(C_)                            \
+  switch (mode) {                                  \
+    case kDirect: MULTI_TWO_PASS(kDirect, C_); break; \
+    case kAdaptT: MULTI_TWO_PASS(kAdaptT, C_); break; \
+    case kAdaptZ: MULTI_TWO_PASS(kAdaptZ, C_); break; \
+    default: MULTI_TWO_PASS(kAdaptTZ, C_); break;     \
+  }
+  if (evals) {
+    MULTI_MODES(true)
+  } else {
+    MULTI_MODES(false)
+  }
+#undef MULTI_MODES
+#undef MULTI_TWO_PASS
+  hipLaunchKernelGGL(lp_sum_kernel, dim3(blocks_for(n)), dim3(kBlock), 0, s, lp, n, part, zeros);
 }
 
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,

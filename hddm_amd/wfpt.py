@@ -82,18 +82,16 @@ def prob_ub(v, a, z):
     return (np.exp(-2 * a * z * v) - 1) / (np.exp(-2 * a * v) - 1)
 
 
-def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=10,
-                      use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0):
-    x = _check_x(x)
-    if multi is None:
-        return full_pdf(x, v, sv, a, z, sz, t, st, err)  # wfpt.pyx:255-256 (TypeError for arrays)
+def _multi_args(n, v, sv, a, z, sz, t, st, multi):
+    """Per-trial arrays (pointer table, kept alive) and scalars of a
+    wiener_like_multi call (wfpt.pyx:257-260: names in `multi` are indexed per
+    trial, the others are scalars)."""
     names = ("v", "sv", "a", "z", "sz", "t", "st")
     vals = (v, sv, a, z, sz, t, st)
     multi = set(multi)
     keep = []
     ptrs = (_lib._PD * 7)()
     scal = np.zeros(7)
-    n = x.shape[0]
     for j, (nm, val) in enumerate(zip(names, vals)):
         if nm in multi:
             arr = np.ascontiguousarray(np.asarray(val, dtype=np.float64))
@@ -104,11 +102,22 @@ def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=
         else:
             ptrs[j] = _lib._PD()
             scal[j] = float(val)
+    return ptrs, scal, keep
+
+
+def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=10,
+                      use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0):
+    x = _check_x(x)
+    if multi is None:
+        return full_pdf(x, v, sv, a, z, sz, t, st, err)  # wfpt.pyx:255-256 (TypeError for arrays)
+    n = x.shape[0]
+    ptrs, scal, keep = _multi_args(n, v, sv, a, z, sz, t, st, multi)
     c = _lib.context()
     K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
     out = ctypes.c_double()
     _lib.check(_lib.wfpt_wiener_like_multi(c.handle, _lib.dptr(x), n, ptrs, _lib.dptr(scal),
                                            ctypes.byref(K), float(p_outlier), ctypes.byref(out)))
+    del keep
     return out.value
 
 
@@ -141,10 +150,12 @@ class Dataset:
     parameters change per proposal). Optional `node_id` groups trials into
     `n_nodes` likelihood nodes scored together by `wiener_like_nodes`."""
 
-    def __init__(self, rt, node_id=None, n_nodes=None, device=None, ctx=None):
+    def __init__(self, rt, node_id=None, n_nodes=None, device=None, ctx=None, input_order=False):
         rt = np.ascontiguousarray(np.asarray(rt, dtype=np.float64).ravel())
         self.ctx = ctx if ctx is not None else _lib.context(device)
         self.n = rt.shape[0]
+        self.input_order = bool(input_order)
+        flags = _lib.WFPT_DS_INPUT_ORDER if input_order else 0
         h = _lib._VP()
         if node_id is not None:
             node = np.ascontiguousarray(np.asarray(node_id, dtype=np.int32).ravel())
@@ -152,14 +163,14 @@ class Dataset:
                 raise ValueError("node_id must have one entry per trial")
             self.n_nodes = int(n_nodes if n_nodes is not None else (node.max() + 1 if node.size
                                                                     else 0))
-            _lib.check(_lib.wfpt_dataset_create(
+            _lib.check(_lib.wfpt_dataset_create_ex(
                 self.ctx.handle, _lib.dptr(rt), self.n,
-                node.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self.n_nodes,
+                node.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), self.n_nodes, flags,
                 ctypes.byref(h)))
         else:
             self.n_nodes = 0
-            _lib.check(_lib.wfpt_dataset_create(self.ctx.handle, _lib.dptr(rt), self.n, None, 0,
-                                                ctypes.byref(h)))
+            _lib.check(_lib.wfpt_dataset_create_ex(self.ctx.handle, _lib.dptr(rt), self.n, None,
+                                                   0, flags, ctypes.byref(h)))
         self.handle = h
 
     def close(self):
@@ -203,6 +214,20 @@ class Dataset:
         _lib.check(_lib.wfpt_wiener_like_allreduce(self.ctx.handle, self.handle,
                                                    ctypes.byref(P), ctypes.byref(K),
                                                    ctypes.byref(out)))
+        return out.value
+
+    def wiener_like_multi(self, v, sv, a, z, sz, t, st, err, multi, n_st=10, n_sz=10,
+                          use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0):
+        """wiener_like_multi (wfpt.pyx:244-274) over this resident dataset
+        (created with input_order=True): only the per-trial parameter arrays
+        go to the device per call."""
+        ptrs, scal, keep = _multi_args(self.n, v, sv, a, z, sz, t, st, multi)
+        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        out = ctypes.c_double()
+        _lib.check(_lib.wfpt_wiener_like_multi_resident(
+            self.ctx.handle, self.handle, ptrs, _lib.dptr(scal), ctypes.byref(K),
+            float(p_outlier), ctypes.byref(out)))
+        del keep
         return out.value
 
     def wiener_like_nodes(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,

@@ -81,6 +81,12 @@ const char *wfpt_last_error(void);
  * The caller's arrays are not retained. */
 int wfpt_dataset_create(wfpt_ctx *ctx, const double *rt, int64_t n, const int32_t *node_id,
                         int32_t n_nodes, wfpt_ds **out);
+/* As wfpt_dataset_create; flags: WFPT_DS_INPUT_ORDER keeps the trials in the
+ * caller's order (no |rt| ordering), as wfpt_wiener_like_multi_resident's
+ * per-trial parameter arrays require. */
+#define WFPT_DS_INPUT_ORDER 1
+int wfpt_dataset_create_ex(wfpt_ctx *ctx, const double *rt, int64_t n, const int32_t *node_id,
+                           int32_t n_nodes, int flags, wfpt_ds **out);
 void wfpt_dataset_destroy(wfpt_ds *ds);
 int64_t wfpt_dataset_size(const wfpt_ds *ds);
 /* The i-th rank's contiguous shard [lo, hi) of n trials (multi-GPU). */
@@ -109,6 +115,12 @@ int wfpt_full_pdf(wfpt_ctx *ctx, double x, const wfpt_params *p, const wfpt_knob
 int wfpt_wiener_like_multi(wfpt_ctx *ctx, const double *x, int64_t n,
                            const double *const arrays[7], const double scalars[7],
                            const wfpt_knobs *k, double p_outlier, double *out_logp);
+/* Same over a resident dataset created with WFPT_DS_INPUT_ORDER (the RTs of a
+ * regression model stay fixed across MCMC; only the per-trial parameter
+ * arrays, hddm_regression.py:26-36, go up per call). */
+int wfpt_wiener_like_multi_resident(wfpt_ctx *ctx, const wfpt_ds *ds,
+                                    const double *const arrays[7], const double scalars[7],
+                                    const wfpt_knobs *k, double p_outlier, double *out_logp);
 
 /* ---- DMAT / Tuerlinckx CDF ---------------------------------------------- */
 /* Per-trial CDF of signed RTs with the outlier mixture, exactly

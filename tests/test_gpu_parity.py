@@ -269,6 +269,52 @@ def test_wiener_like_multi(gpu, oracle_lib):
         assert abs(got - ref) < 1e-9 * abs(ref)
 
 
+@pytest.mark.parametrize("case", ["adapt_tz", "direct", "adapt_t", "adapt_z", "generic_sz",
+                                  "heavy"])
+def test_wiener_like_multi_families(gpu, oracle_lib, case):
+    """wiener_like_multi's level-0 fast path for every uniform family (sz, st
+    scalar) incl. a refinement-heavy parameter set (deferred records), and the
+    generic per-trial kernel (sz per trial); host and resident datasets; the
+    +-999 missing responses. Total vs the reference restated (oracle, pinned to
+    the reference's kernels), relative 1e-10."""
+    rng = np.random.default_rng(17)
+    n = 20000
+    x = rng.choice([-1.0, 1.0], n) * (0.3 + rng.gamma(2.0, 0.4, n))
+    x[::101] = 999.0
+    x[::103] = -999.0
+    v = rng.uniform(-1.5, 1.5, n)
+    a = rng.uniform(0.8, 2.2, n)
+    z = rng.uniform(0.4, 0.6, n)
+    sz_arr = rng.uniform(0.0, 0.3, n)
+    base = dict(v=v, sv=0.3, a=a, z=0.5, sz=0.1, t=0.25, st=0.1)
+    multi = ["v", "a"]
+    kn = dict(n_st=2, n_sz=2, simps_err=1e-3, p_outlier=0.05, w_outlier=0.1)
+    if case == "direct":
+        base.update(sz=0.0, st=0.0, sv=0.0)
+    elif case == "adapt_t":
+        base.update(sz=0.0)
+    elif case == "adapt_z":
+        base.update(st=0.0, z=z)
+        multi = ["v", "a", "z"]
+    elif case == "generic_sz":
+        base.update(sz=sz_arr)
+        multi = ["v", "a", "sz"]
+    elif case == "heavy":
+        base.update(sv=2.0, sz=0.35, st=0.3)
+        kn.update(simps_err=1e-6, n_st=4, n_sz=4)
+        x = np.where(np.abs(x) < 998, np.sign(x) * (0.16 + 0.3 * rng.random(n)), x)
+    args = [base[k] for k in ("v", "sv", "a", "z", "sz", "t", "st")]
+    ref = oracle_lib.wiener_like_multi(x, *args, 1e-4, multi=multi, **kn)
+    tol = 1e-10 * abs(ref)  # every term is negative: |sum| = sum |terms|
+    got = gpu.wiener_like_multi(x, *args, 1e-4, multi=multi, **kn)
+    assert np.isfinite(ref) and abs(got - ref) <= tol, (case, got, ref)
+    ds = gpu.Dataset(x, input_order=True)
+    got2 = ds.wiener_like_multi(*args, 1e-4, multi, **kn)
+    assert got2 == got, (got2, got)
+    with pytest.raises(ValueError):
+        gpu.Dataset(x).wiener_like_multi(*args, 1e-4, multi, **kn)
+
+
 def test_gen_rts_from_cdf(gpu):
     np.random.seed(5)
     rts = gpu.gen_rts_from_cdf(0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1, samples=20000, dt=1e-3)

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--burn", type=int, default=20)
     ap.add_argument("--full", action="store_true", help="include sv, sz, st (full DDM)")
+    ap.add_argument("--progress", type=int, default=0)
+    ap.add_argument("--json", default=None, help="also write the JSON line here")
     a = ap.parse_args()
     from hddm_amd.hierarchical import HDDM, gen_data
     t0 = time.perf_counter()
@@ -40,10 +42,10 @@ def main():
     t_gen = time.perf_counter() - t0
     m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st") if a.full else (),
              seed=1)
-    m.sample(a.burn)  # warm-up (untimed)
+    m.sample(a.burn, progress=a.progress or None)  # burn-in (untimed)
     c0, s0 = m.likelihood_calls, m.likelihood_seconds
     t0 = time.perf_counter()
-    m.sample(a.iters)
+    m.sample(a.iters, progress=a.progress or None)
     el = time.perf_counter() - t0
     calls = m.likelihood_calls - c0
     lik_s = m.likelihood_seconds - s0
@@ -62,29 +64,37 @@ def main():
         "trial_evals_per_s": calls * m.n_trials / el,
         "data_generation_s": t_gen,
         "posterior": {k: stats[k]["mean"] for k in stats},
+        "posterior_95": {k: [stats[k]["2.5q"], stats[k]["97.5q"]] for k in stats},
         "truth": {"a": float(np.mean(truth["a"])), "t": float(np.mean(truth["t"])),
                   "v(c0)": float(np.mean(truth["v"]["c0"])),
-                  "v(c1)": float(np.mean(truth["v"]["c1"]))},
+                  "v(c1)": float(np.mean(truth["v"]["c1"])), "sv": sv, "sz": sz, "st": st},
+        "subject_recovery": {
+            f: float(np.corrcoef(np.mean(m.trace_subj[f], axis=0)[::len(m.levels[f])],
+                                 np.asarray(truth[f] if f != "v" else truth["v"]["c0"]))[0, 1])
+            for f in ("a", "t", "v")},
+        "burn": a.burn,
     }
-    try:
-        import oracle
-        R = oracle.load_ref()
-        if R is not None:
-            node = data["rt"].to_numpy()[: a.trials // 2]
-            p = (1.0, sv, 2.0, 0.5, sz, 0.3, st)
-            reps, t1 = 0, time.perf_counter()
-            while time.perf_counter() - t1 < 2.0:
-                R.wiener_like(node, *p, 1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
-                reps += 1
-            per_node = (time.perf_counter() - t1) / reps
-            out["cpu_reference_estimate"] = {
-                "per_node_call_s": per_node, "node_size": int(node.size),
-                "likelihood_s_per_sweep": per_node * node_evals / a.iters,
-                "note": "reference Cython wiener_like per node x node evaluations of one sweep; "
-                        "excludes PyMC/kabuki overhead (not runnable offline)"}
-    except Exception as e:  # noqa: BLE001
-        out["cpu_reference_estimate"] = {"error": str(e)}
-    print(json.dumps(out), flush=True)
+    # the reference's CPU cost of the same node evaluations: the C restatement
+    # of wiener_like (oracle/wfpt_oracle.c, calibrated 1.0x against the
+    # reference's own kernels, profiles/r02/cpu_calibration.json), 1 thread
+    import oracle
+    node = data["rt"].to_numpy()[: a.trials // 2].copy()
+    p = (1.0, sv, 2.0, 0.5, sz, 0.3, st)
+    reps, t1 = 0, time.perf_counter()
+    while time.perf_counter() - t1 < 2.0:
+        oracle.wiener_like(node, *p, 1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+        reps += 1
+    per_node = (time.perf_counter() - t1) / reps
+    out["cpu_port_estimate"] = {
+        "per_node_call_s": per_node, "node_size": int(node.size), "kind": "port", "cores": 1,
+        "likelihood_s_per_sweep": per_node * node_evals / a.iters,
+        "note": "C restatement of the reference's wiener_like per node x the node evaluations "
+                "of one sweep; excludes PyMC/kabuki overhead (not runnable offline)"}
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.json:
+        with open(a.json, "w") as fh:
+            fh.write(line + "\n")
 
 
 if __name__ == "__main__":
