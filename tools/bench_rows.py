@@ -66,7 +66,13 @@ def main():
     a = ap.parse_args()
     import oracle
     from hddm_amd import _lib, cdfdif_wrapper, wfpt
-    R = oracle.load_ref()
+    # CPU baselines: the C restatement of the reference's kernels (kind "port",
+    # oracle/wfpt_oracle.c; calibrated 0.87-1.01x against the reference's own
+    # compiled kernels in the build container, profiles/r02/cpu_calibration.json),
+    # 1 thread. The reference's compiled cdfdif exists only in the build
+    # container (oracle/_ref never travels), so the CDF row has a CPU number
+    # only there.
+    R = oracle
     C = oracle.load_ref_cdfdif()
     ctx = _lib.context(0)
     np.random.seed(20261015)
@@ -81,7 +87,7 @@ def main():
     ref = cpu_rate(lambda: R.pdf_array(x, *SIMPLE, 1e-4, 1), x.size, cs) if R else None
     emit({"row": "C1 pdf_array simple 10k (host in/out, PCIe incl.)", "trials": x.size,
           "gpu_call_us": wall * 1e6, "gpu_trials_per_s": x.size / wall,
-          "cpu_ref_trials_per_s": ref})
+          "cpu_port_trials_per_s": ref})
 
     # C2: simple DDM, 10M resident trials, wiener_like
     x10 = np.tile(x_simple, 10)
@@ -92,7 +98,7 @@ def main():
     ref = cpu_rate(lambda: R.wiener_like(s, *SIMPLE, *KN), s.size, cs) if R else None
     emit({"row": "C2 wiener_like simple 10M resident", "trials": x10.size, "kernel_ms": k,
           "call_ms": wall * 1e3, "gpu_trials_per_s": x10.size / wall,
-          "cpu_ref_trials_per_s": ref})
+          "cpu_port_trials_per_s": ref})
     del ds
 
     # C3: full DDM, 1M resident (the headline; also PCIe-inclusive host path)
@@ -105,7 +111,7 @@ def main():
     emit({"row": "C3 wiener_like full DDM 1M", "trials": x_full.size, "kernel_ms": k,
           "call_ms_resident": wall * 1e3, "call_ms_host_array": wall_h * 1e3,
           "gpu_trials_per_s": x_full.size / wall,
-          "gpu_trials_per_s_pcie_incl": x_full.size / wall_h, "cpu_ref_trials_per_s": ref})
+          "gpu_trials_per_s_pcie_incl": x_full.size / wall_h, "cpu_port_trials_per_s": ref})
     del ds
 
     # stress: random parameter sets (hddm/generate.py:38-46 ranges), 4 x 250k
@@ -139,7 +145,7 @@ def main():
         ref_call = per * n_nodes
     emit({"row": "(f)1 wiener_like_nodes simple 400 nodes x 250 (one batched call)",
           "trials": node.size, "kernel_ms": k, "call_ms": wall * 1e3,
-          "cpu_ref_ms_for_400_node_calls": ref_call and ref_call * 1e3})
+          "cpu_port_ms_for_400_node_calls": ref_call and ref_call * 1e3})
     Pf = P.copy()
     Pf[:, 1], Pf[:, 4], Pf[:, 6] = 0.1, 0.1, 0.1
     k = gpu_kernel_ms(ctx, lambda: dsn.wiener_like_nodes(Pf))
@@ -149,7 +155,7 @@ def main():
         ref_call = per * n_nodes
     emit({"row": "(f)1 wiener_like_nodes full DDM 400 nodes x 250", "trials": node.size,
           "kernel_ms": k, "call_ms": wall * 1e3,
-          "cpu_ref_ms_for_400_node_calls": ref_call and ref_call * 1e3})
+          "cpu_port_ms_for_400_node_calls": ref_call and ref_call * 1e3})
     del dsn
 
     # (f)2: wiener_like_multi, per-trial v and a, 1M (host arrays)
@@ -170,6 +176,16 @@ def main():
     emit({"row": "(f)2 wiener_like_multi full DDM 1M (v, a per trial; host arrays)",
           "trials": xm.size, "call_ms": wall * 1e3, "gpu_trials_per_s": xm.size / wall,
           "cpu_port_trials_per_s": ref})
+    # resident RTs (input order), per-trial v and a uploaded per call
+    dsm = wfpt.Dataset(xm, input_order=True)
+    g = lambda: dsm.wiener_like_multi(vm, 0.1, am, 0.5, 0.1, 0.3, 0.1, 1e-4, ["v", "a"], n_st=2,
+                                      n_sz=2, simps_err=1e-3, p_outlier=0.05, w_outlier=0.1)
+    k = gpu_kernel_ms(ctx, g, reps=5)
+    wall = timed(g)
+    emit({"row": "(f)2 wiener_like_multi full DDM 1M (resident RTs, v and a per trial uploaded "
+                 "per call)", "trials": xm.size, "kernel_ms": k, "call_ms": wall * 1e3,
+          "gpu_trials_per_s": xm.size / wall, "cpu_port_trials_per_s": ref})
+    del dsm
 
     # (f)3: gen_rts_from_cdf (density grid on GPU), 1M samples, dt 1e-3
     wall = timed(lambda: wfpt.gen_rts_from_cdf(*FULL, samples=1_000_000, dt=1e-3), min_reps=2)
