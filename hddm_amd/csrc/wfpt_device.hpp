@@ -137,6 +137,8 @@ __host__ __device__ inline void sincospi01(double w, double& s, double& c) {
   }
 }
 
+constexpr double kInvSqrt2Pi = 0.398942280401432677939946059934;  // 1 / sqrt(2 pi)
+
 struct TNode {
   double xx;    // x - t_node: the `x` argument of pdf_sv
   double tt;    // xx / a^2 (pdf.pxi:98)
@@ -234,9 +236,13 @@ __device__ inline Decision decide64(double tt, double err) {
 // qhint >= 0: exp(-pi^2 tt / 2) of this node computed by the caller (a
 // recurrence over the t grid); < 0: computed here. has_known: `known` is the
 // node's decision, established by the caller (shared over a trial's t grid).
-__device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err,
-                                    double qhint = -1.0, bool has_known = false,
-                                    Decision known = Decision{0, 0, 0}) {
+// ia2: 1 / a^2 of the call, computed once by the caller. tt comes from a
+// product: it feeds the fp32 decision estimate (1e-5 guard band) and values
+// only; the fp64 decision, reached near a threshold, divides exactly as
+// pdf.pxi:98.
+__device__ inline TNode tnode_setup_r(double xx, double v, double sv, double a, double ia2,
+                                      double err, double qhint = -1.0, bool has_known = false,
+                                      Decision known = Decision{0, 0, 0}) {
   TNode T;
   T.xx = xx;
   T.pos = xx > 0;
@@ -252,18 +258,20 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   T.amb = 0;
   if (!T.pos) return T;
   const double a2 = a * a;
-  const double tt = xx / a2;
+  const double tt = xx * ia2;
   T.tt = tt;
   Decision D;
   float args;
   if (has_known) D = known;
-  else if (!decide32(tt, err, D, args)) D = decide64(tt, err);
+  else if (!decide32(tt, err, D, args)) D = decide64(xx / a2, err);
   T.amb = D.amb;
   if (D.small) {
     T.small = 1;
     T.K = D.K;
-    T.rn = rsqrt((2.0 * kPi) * ((tt * tt) * tt));  // value only: 1/sqrt(2 pi tt^3)
-    T.m = -0.5 / tt;
+    // values only: 1/sqrt(2 pi tt^3) and -1/(2 tt) from one rsqrt
+    const double r = rsqrt(tt), r2 = r * r;
+    T.rn = kInvSqrt2Pi * (r2 * r);
+    T.m = -0.5 * r2;
   } else {
     T.small = 0;
     T.K = D.K;
@@ -271,7 +279,7 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
     T.q2 = T.m * T.m;
   }
   // values only: 1/(2u) and 1/(a^2 sqrt(u)), u = sv^2 xx + 1, from one rsqrt
-  T.sc = 1.0 / a2;
+  T.sc = ia2;
   if (sv != 0) {
     const double r = rsqrt(((sv * sv) * xx) + 1.0);
     T.cden = (0.5 * r) * r;
@@ -279,6 +287,35 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
   }
   T.vvx = (v * v) * xx;
   return T;
+}
+__device__ inline TNode tnode_setup(double xx, double v, double sv, double a, double err,
+                                    double qhint = -1.0, bool has_known = false,
+                                    Decision known = Decision{0, 0, 0}) {
+  return tnode_setup_r(xx, v, sv, a, 1.0 / (a * a), err, qhint, has_known, known);
+}
+
+// Series accumulation c + a b. Values only (never a decision input: the series
+// choice, K and the Simpson stop tests use the reference's operations, and a
+// stop test within kTieBand = 1e-11 of its threshold is re-decided on the exact
+// path), so one fused rounding instead of two is within the few-ulp value
+// error the recurrences already carry. WFPT_SERIES_FMA=0 restores mul + add.
+#ifndef WFPT_SERIES_FMA
+#define WFPT_SERIES_FMA 1
+#endif
+__device__ inline double madd(double a, double b, double c) {
+#if WFPT_SERIES_FMA
+  return fma(a, b, c);
+#else
+  return c + a * b;
+#endif
+}
+// a b - c (the Chebyshev step 2cos(pi w) sin(k pi w) - sin((k-1) pi w))
+__device__ inline double msub(double a, double b, double c) {
+#if WFPT_SERIES_FMA
+  return fma(a, b, -c);
+#else
+  return a * b - c;
+#endif
 }
 
 // f(t|0,1,w) from a prepared t node (pdf.pxi:49-65).
@@ -290,7 +327,7 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
     const int upper = (int)ceil((K - 1) / 2.);
     for (int k = lower; k <= upper; ++k) {
       const double wk = w + (double)(2 * k);
-      p = p + wk * exp((wk * wk) * T.m);
+      p = madd(wk, exp((wk * wk) * T.m), p);
     }
     p = p * T.rn;
   } else {
@@ -301,12 +338,12 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
     double e = T.m, r = T.m * T.q2;      // q^(k^2), q^(2k+1)
     if (K >= 1) p = e * s1;
     for (int k = 2; k <= K; ++k) {
-      const double sn = tc * sk - skm1;
+      const double sn = msub(tc, sk, skm1);
       skm1 = sk;
       sk = sn;
       e = e * r;
       r = r * T.q2;
-      p = p + ((double)k * e) * sk;
+      p = madd((double)k * e, sk, p);
     }
     p = p * kPi;
   }
@@ -778,6 +815,7 @@ struct ZGrid {
   double g[5];
   double s0, c0, s4, c4, sd, cd;
   double A[5];
+  double h6, h12;  // (g4 - g0) / 6 and / 12: the Simpson weights of this grid's interval
 };
 
 __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, double a) {
@@ -800,6 +838,8 @@ __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, d
       G.A[i] = (azsv * azsv) - (((2.0 * a) * v) * G.g[i]);
     }
   }
+  G.h6 = (G.g[4] - G.g[0]) / 6;
+  G.h12 = (G.g[4] - G.g[0]) / 12;
   return G;
 }
 
@@ -846,13 +886,13 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
         double R = exp(d1);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-          p[i] = p[i] + wk[i] * E;
+          p[i] = madd(wk[i], E, p[i]);
           E = E * R;
           R = R * qq;
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) p[i] = p[i] + wk[i] * exp(ek[i]);
+        for (int i = 0; i < 5; ++i) p[i] = madd(wk[i], exp(ek[i]), p[i]);
       }
     }
 #pragma unroll
@@ -888,17 +928,17 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
       const double ke1 = (double)(k + 1) * e;
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        skm1[i] = tc[i] * sk[i] - skm1[i];  // sin(k pi w)
-        p[i] = p[i] + ke * skm1[i];
-        sk[i] = tc[i] * skm1[i] - sk[i];    // sin((k+1) pi w)
-        p[i] = p[i] + ke1 * sk[i];
+        skm1[i] = msub(tc[i], sk[i], skm1[i]);  // sin(k pi w)
+        p[i] = madd(ke, skm1[i], p[i]);
+        sk[i] = msub(tc[i], skm1[i], sk[i]);    // sin((k+1) pi w)
+        p[i] = madd(ke1, sk[i], p[i]);
       }
     }
     if (k <= K) {
       e = e * r;
       const double ke = (double)k * e;
 #pragma unroll
-      for (int i = 0; i < 5; ++i) p[i] = p[i] + ke * (tc[i] * sk[i] - skm1[i]);
+      for (int i = 0; i < 5; ++i) p[i] = madd(ke, msub(tc[i], sk[i], skm1[i]), p[i]);
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = p[i] * kPi;
@@ -971,6 +1011,25 @@ __host__ __device__ inline Simp simp5(double h, double fb, double fd, double fm,
   return s;
 }
 
+// simp5 with the interval's weights h/6, h/12 precomputed (the same IEEE
+// divisions of the same h: bit-identical).
+__device__ inline Simp simp5p(double h6, double h12, double fb, double fd, double fm, double fe,
+                              double fu) {
+  Simp s;
+  s.S = h6 * ((fb + (4 * fm)) + fu);
+  s.Sl = h12 * ((fb + (4 * fd)) + fm);
+  s.Sr = h12 * ((fm + (4 * fe)) + fu);
+  s.S2 = s.Sl + s.Sr;
+  return s;
+}
+// The leaf value S2 + (S2 - S) / 15 of an interval that stops refining
+// (integrate.pxi:106,171), with 1/15 as a product: a value, never a decision
+// input at its own level (the stop test reads S and S2), within an ulp of the
+// quotient. Every site that must produce the same bits for a t node's root z
+// integral (inner_root, the engine's task completion) uses this.
+constexpr double kInv15 = 1.0 / 15.0;
+__device__ inline double simp_value(const Simp& s) { return s.S2 + (s.S2 - s.S) * kInv15; }
+
 // The z integral at one t node (adaptiveSimpsons_1D over z, integrate.pxi:
 // 114-141), root level only: the root's 5 evaluations 5-wide on the grid and
 // its stop test. repair = the test asks for refinement (the value is then the
@@ -983,9 +1042,9 @@ __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, 
 #pragma unroll
   for (int i = 0; i < 5; ++i) f[i] = f[i] * iZz;
   ne += 5;
-  const Simp s = simp5(G.g[4] - G.g[0], f[0], f[1], f[2], f[3], f[4]);
+  const Simp s = simp5p(G.h6, G.h12, f[0], f[1], f[2], f[3], f[4]);
   repair = simpson_refine(s.S, s.S2, K.simps_err, K.n_sz, flags);
-  return s.S2 + (s.S2 - s.S) / 15;
+  return simp_value(s);
 }
 
 // Root interval of the adaptive tree: over t for kAdaptT / kAdaptTZ, over z
@@ -1122,6 +1181,7 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
 // (EngTables), shared by both.
 struct L0Hints {
   double qn[5];
+  double ia2;  // 1 / a^2
   Decision D0, D4;
   bool ok0, ok4, shared;
 };
@@ -1133,8 +1193,11 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
   H.D4 = Decision{0, 0, 0};
   H.ok0 = H.ok4 = H.shared = false;
   const double a2 = a * a;
-  const double q0 = exp((-kPi2 * ((x - lb) / a2)) / 2.0);
-  const double R = exp((kPi2 * (ub - lb)) / (8.0 * a2));
+  const double ia2 = 1.0 / a2;
+  H.ia2 = ia2;
+  // values only (the fp32 decision estimates below have a 1e-5 guard band)
+  const double q0 = exp((-kPi2 * ((x - lb) * ia2)) * 0.5);
+  const double R = exp((kPi2 * (ub - lb)) * (0.125 * ia2));
   if (q0 > 1e-280 && R < 1e10 && x - lb > 0) {
     const double R2 = R * R;
     H.qn[0] = q0;
@@ -1145,8 +1208,8 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
   }
   if (x - ub > 0) {
     float args0, args4;
-    H.ok0 = decide32((x - lb) / a2, err, H.D0, args0);
-    H.ok4 = decide32((x - ub) / a2, err, H.D4, args4);
+    H.ok0 = decide32((x - lb) * ia2, err, H.D0, args0);
+    H.ok4 = decide32((x - ub) * ia2, err, H.D4, args4);
     H.shared = H.ok0 && H.ok4 && args0 < 0.5f && H.D0.small == H.D4.small && H.D0.K == H.D4.K;
   }
   return H;
@@ -1168,7 +1231,7 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
   const double qh =
       j == 0 ? H.qn[0] : j == 1 ? H.qn[1] : j == 2 ? H.qn[2] : j == 3 ? H.qn[3] : H.qn[4];
   const bool known = j == 0 ? H.ok0 : (j == 4 ? H.ok4 : H.shared);
-  const TNode T = tnode_setup(x - tc, v, sv, a, err, qh, known, j == 4 ? H.D4 : H.D0);
+  const TNode T = tnode_setup_r(x - tc, v, sv, a, H.ia2, err, qh, known, j == 4 ? H.D4 : H.D0);
   pend = false;
   if (T.amb) {
     flags |= kFlagExact;
@@ -1280,6 +1343,8 @@ __host__ __device__ inline ZGrid zgrid_of(double lb, double ub, int sel, double 
       G.A[i] = (azsv * azsv) - (((2.0 * a) * v) * G.g[i]);
     }
   }
+  G.h6 = (G.g[4] - G.g[0]) / 6;
+  G.h12 = (G.g[4] - G.g[0]) / 12;
   return G;
 }
 

@@ -324,6 +324,7 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
   const int nsz = A.K.n_sz;
   const int depth = (MODE == kAdaptZ) ? A.K.n_sz : A.K.n_st;
   const double iwt = 1.0 / (cl.tab.tP[kTreeW] - cl.tab.tP[0]);
+  const double ia2 = 1.0 / (a * a);  // as l0_hints: the same tt for the same t node
   int L = 0, r = 0;
 #pragma unroll 1
   for (;;) {
@@ -427,7 +428,7 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
         known = j == 0 ? H.ok0 : (j == 4 ? H.ok4 : H.shared);
         kd = j == 4 ? H.D4 : H.D0;
       }
-      const TNode T = tnode_setup(xx, vo, sv, a, err, qh, known, kd);
+      const TNode T = tnode_setup_r(xx, vo, sv, a, ia2, err, qh, known, kd);
       if (T.amb) atomicOr(&cl.fl[owner], (int)kFlagExact);
       if (MODE == kAdaptT) y[0] = tnode_pdf_sv(T, flip ? 1. - z : z, vo, sv, a);
       else tnode_pdf_sv_grid5(T, cl.tab.G[flip][gs], vo, sv, a, y);
@@ -447,13 +448,15 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
         } else {
           // kAdaptTZ: the z integral's prologue + root test (integrate.pxi:
           // 114-141); a refinement queues the z walk
+          // (inner_root's operations: the root grid's weights, simp_value)
           const double izf = cl.tab.iz[flip];
-          const double hz = cl.tab.zP[flip][kTreeW] - cl.tab.zP[flip][0];
-          const Simp s = simp5(hz, y[0] * izf, y[1] * izf, y[2] * izf, y[3] * izf, y[4] * izf);
+          const ZGrid& gr = cl.tab.G[flip][kGridRoot];
+          const Simp s = simp5p(gr.h6, gr.h12, y[0] * izf, y[1] * izf, y[2] * izf, y[3] * izf,
+                                y[4] * izf);
           int f = 0;
           pend = simpson_refine(s.S, s.S2, se, nsz, f);
           if (f) atomicOr(&cl.fl[owner], f);
-          else if (!pend) cl.F[pos * 64 + owner] = (s.S2 + (s.S2 - s.S) / 15) * iwt;
+          else if (!pend) cl.F[pos * 64 + owner] = simp_value(s) * iwt;
           if (COUNT) atomicAdd(&cl.cnt[owner], 5);
         }
       }
@@ -632,7 +635,6 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
 #ifdef WFPT_PHASE_TIMING
   const long long rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  load_tables(cl, tab, lane);
   // work units: the split chunks' units first (dispatched first), then one
   // wave per chunk
   const int64_t u = (int64_t)blockIdx.x * kEngWaves + (threadIdx.x >> 6);
@@ -641,6 +643,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
   const int64_t c = split ? (int64_t)S.list[slot] : u - (int64_t)S.n * kSplit;
   if (!split && (c * 64 >= A.n || (S.n > 0 && S.pred[c]))) return;  // past the end / split
   if (W.redo && !W.redo[c]) return;  // redo pass: only the chunks the lean pass flagged
+  load_tables(cl, tab, lane);
   const int64_t i = split ? c * 64 + sub * kSplitTrials + lane : c * 64 + lane;
   const bool own = (split ? lane < kSplitTrials : true) && i < A.n;
   const double x0 = own ? A.x[i] : 0.0;
@@ -751,6 +754,8 @@ __device__ inline ZGrid zgrid_pick(const RootGrids& R, bool pos) {
     G.g[k] = pos ? g1.g[k] : g0.g[k];
     G.A[k] = pos ? g1.A[k] : g0.A[k];
   }
+  G.h6 = pos ? g1.h6 : g0.h6;
+  G.h12 = pos ? g1.h12 : g0.h12;
   G.s0 = pos ? g1.s0 : g0.s0;
   G.c0 = pos ? g1.c0 : g0.c0;
   G.s4 = pos ? g1.s4 : g0.s4;
