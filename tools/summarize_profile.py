@@ -79,10 +79,10 @@ def main():
         json.dump(summary, fh, indent=1)
     shutil.copy(os.path.join(PROF, "trace", "trace_kernel_stats.csv"),
                 os.path.join(out_dir, "kernel_stats.csv"))
-    import sys
-    sys.path.insert(0, ROOT)
-    from hddm_amd import build as hb
-    sha = hb.built_digest()
+    # the digest of the library the GPU run profiled (tools/gpu_profile.sh
+    # records it next to the counters), not whatever is built here now
+    with open(os.path.join(PROF, "src_sha1.txt")) as fh:
+        sha = fh.read().strip()
     summary["src_sha1"] = sha
     with open(os.path.join(out_dir, "pmc_summary.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
