@@ -134,3 +134,27 @@ def test_rccl_single_rank_allreduce_path(gpu, oracle_lib):
     x[17] = 0.1
     ds0 = gpu.Dataset(x)
     assert ds0.wiener_like_allreduce(*args, 1e-4, 2, 2, 1, 1e-3, 0.0, 0.1) == -math.inf
+
+
+@pytest.mark.gpu
+def test_rccl_allreduce_call_sequences(gpu):
+    """Repeated all-reduce calls take the predicted sequences (lean level-0
+    pass + unconditional redo pass once the dataset's last call refined
+    nothing in-wave): bitwise the local wiener_like result, also when a call
+    with refining parameters follows non-refining ones (redo inside the same
+    launch sequence, no host round trip before the exchange)."""
+    from hddm_amd import _lib, dist as hdist
+    ctx = _lib.context()
+    hdist.init_comm(ctx, 0, 1)
+    np.random.seed(4)
+    calm = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    heavy = (1.7431, 2.0137, 0.6119, 0.5386, 0.2108, 0.3567, 0.1981)
+    x = gpu.gen_rts_from_cdf(*heavy, samples=100_000, dt=1e-3)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    ds = gpu.Dataset(x)
+    ref_calm = gpu.Dataset(x).wiener_like(*calm, *kn)
+    ref_heavy = gpu.Dataset(x).wiener_like(*heavy, *kn)
+    seq = [calm, calm, calm, heavy, heavy, calm, calm, heavy]
+    for p in seq:
+        got = ds.wiener_like_allreduce(*p, *kn)
+        assert got == (ref_calm if p is calm else ref_heavy), p
