@@ -790,6 +790,110 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   chunk_out<COUNT, OUT>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
 }
 
+// A node's trial term: mixture with the node's p_outlier, -inf for a zero
+// density or a p_outlier outside [0, 1] (wfpt.pyx:63-72 per node).
+__device__ inline double node_logp(double p, const Params& Q, const Knobs& K) {
+  const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);  // wfpt.pyx:63-64 per node
+  p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
+  return (!ok || p == 0) ? -INFINITY : log(p);
+}
+
+// The per-call tables (EngTables) of one trial's parameters, built by the lanes
+// of a wave in parallel: lanes 0-7 the 8 z grids, then the dyadic points of the
+// t tree and of both z trees, then 1 / (ub_z - lb_z). The same functions as
+// the host's eng_tables.
+__device__ inline void eng_tables_wave(const Params& P, EngTables& T, int lane) {
+  constexpr int kP = kTreePoints;
+  if (lane < 8) {
+    const int flip = lane >> 2, sel = lane & 3;
+    const double zf = flip ? 1. - P.z : P.z, vf = flip ? -P.v : P.v;
+    T.G[flip][sel] = zgrid_of(zf - P.sz / 2., zf + P.sz / 2., sel, vf, P.sv, P.a);
+  } else if (lane < 8 + kP) {
+    T.tP[lane - 8] = dyadic_point(P.t - P.st / 2., P.t + P.st / 2., lane - 8);
+  } else if (lane < 8 + 3 * kP) {
+    const int idx = lane - 8 - kP, flip = idx / kP, k = idx % kP;
+    const double zf = flip ? 1. - P.z : P.z;
+    T.zP[flip][k] = dyadic_point(zf - P.sz / 2., zf + P.sz / 2., k);
+  } else if (lane < 8 + 3 * kP + 2) {
+    const int flip = lane - (8 + 3 * kP);
+    const double zf = flip ? 1. - P.z : P.z;
+    T.iz[flip] = 1.0 / ((zf + P.sz / 2.) - (zf - P.sz / 2.));
+  }
+  wave_sync();
+}
+
+// Deferred trials of the per-node and per-trial-parameter paths (records of
+// index + parameter row; adaptive families). The per-lane recursion would
+// leave one lane walking a trial's whole tree serially (~40 dependent
+// evaluations at one-wave latency set the call's length); instead one wave
+// takes one record and runs the engine's breadth-first rounds on the trial's
+// own tables: its level-0 t nodes (or root z grid) as tasks, then refinement
+// levels and z walks across the lanes, exactly as a split unit of the dataset
+// engine. Trees deeper than kTreeDepth and rounding-critical values take the
+// per-lane fallback / exact path on lane 0. MULTI: wiener_like_multi's term.
+template <int MODE, bool COUNT, bool MULTI>
+__global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
+    const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
+    const int* n_defer, unsigned long long* evals, int* status) {
+  __shared__ ChunkLds<1> lds[kEngWaves];
+  const int lane = threadIdx.x & 63;
+  ChunkLds<1>& cl = lds[threadIdx.x >> 6];
+  const int nd = *n_defer;
+  const int nwaves = (int)gridDim.x * kEngWaves;
+  long long ne = 0;
+  int errf = 0;
+  for (int k = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
+       k < nd; k += nwaves) {
+    const int64_t i = d_idx[k];
+    const Params Q = d_par[k];
+    TrialArgs A{};
+    A.x = x;
+    A.P = Q;
+    A.K = K;
+    A.wp_outlier = K.w_outlier * Q.p_outlier;
+    const double x0 = x[i];
+    eng_tables_wave(Q, cl.tab, lane);
+    cl.X[lane] = lane == 0 ? x0 : 0.0;
+    cl.fl[lane] = (lane == 0 && trial_setup(x0, Q).valid) ? 0 : (int)kFlagIdle;
+    if (COUNT) cl.cnt[lane] = 0;
+    if (lane == 0) {
+      cl.qn[0] = 0;
+      cl.qn[1] = 0;
+    }
+    wave_sync();
+    constexpr int n0 = (MODE == kAdaptZ) ? 1 : 5;
+    team_push(lane < n0 && !(cl.fl[0] & kFlagStop), (lane * (kTreeW / 4)) << 6, cl.Q, &cl.qn[0]);
+    wave_sync();
+    Tally ty;
+    PhaseClock pc;
+    refine_rounds<MODE, COUNT, 1>(A, cl, lane, 0, ty, pc);
+    if (lane == 0) {
+      double p = 0.0;
+      bool defer = false;
+      int rf = kFlagExact;
+      long long n1 = 0;
+      if (!(cl.fl[0] & kFlagIdle)) {
+        tree_density<MODE, 1>(A, cl, 0, x0, p, defer, rf);
+        if (COUNT) n1 = cl.cnt[0];
+      }
+      if (defer) {
+        n1 = 0;
+        p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
+                              : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+      }
+      ne += n1;
+      lp[i] = MULTI ? log(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier))
+                    : node_logp(p, Q, K);
+    }
+    wave_sync();  // the next record reuses this wave's LDS
+  }
+  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
+  if (COUNT) {
+    ne = wave_sum_ll(ne);
+    if (lane == 0) atomicAdd(evals, (unsigned long long)ne);
+  }
+}
+
 // Settles every deferred trial and folds it into its chunk: block g walks
 // chunks g, g + G, ... (64 chunk counts per parallel load); a chunk's deferred
 // trials run on its first lanes (the exact path, or the per-lane walk for
@@ -1022,11 +1126,6 @@ struct StackOf {
       typename std::conditional<STK == 1, RegStack<4>, MemStack<WFPT_MAX_DEPTH>>::type>::type;
 };
 
-__device__ inline double node_logp(double p, const Params& Q, const Knobs& K) {
-  const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);  // wfpt.pyx:63-64 per node
-  p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
-  return (!ok || p == 0) ? -INFINITY : log(p);
-}
 
 template <int STK, bool COUNT>
 __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(
@@ -1411,18 +1510,18 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                                   int* status, hipStream_t s) {
   hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
                      node, n, P, K, lp, d_idx, d_par, n_defer, evals, status);
-  const int64_t nl = (n + 63) / 64;
-  const int64_t g = nl < 2048 ? nl : 2048;
-  const int stk = stack_kind(K);
-  if (stk == 0)
+  if constexpr (MODE != kDirect) {
+    // adaptive families: one wave per deferred record (node_engine_kernel)
+    const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 1024);
+    hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, false>), dim3(nb), dim3(kEngBlock), 0, s, x,
+                       K, lp, d_idx, d_par, n_defer, evals, status);
+  } else {
+    // direct family: only exact-path records, one lane each
+    const int64_t nl = (n + 63) / 64;
+    const int64_t g = nl < 2048 ? nl : 2048;
     hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
                        d_idx, d_par, n_defer, evals, status);
-  else if (stk == 1)
-    hipLaunchKernelGGL((node_slow_kernel<MODE, 1, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
-                       d_idx, d_par, n_defer, evals, status);
-  else
-    hipLaunchKernelGGL((node_slow_kernel<MODE, 2, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
-                       d_idx, d_par, n_defer, evals, status);
+  }
 }
 
 template <bool COUNT>
@@ -1486,18 +1585,18 @@ static void launch_multi_two_pass(const double* x, int64_t n, const double* cons
                                   unsigned long long* evals, int* status, hipStream_t s) {
   hipLaunchKernelGGL((multi_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
                      n, arr, scal, K, p_outlier, lp, d_idx, d_par, n_defer, evals);
-  const int64_t nl = (n + 63) / 64;
-  const int64_t g = nl < 2048 ? nl : 2048;
-  const int stk = stack_kind(K);
-  if (stk == 0)
+  if constexpr (MODE != kDirect) {
+    // adaptive families: one wave per deferred record (node_engine_kernel)
+    const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 1024);
+    hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, true>), dim3(nb), dim3(kEngBlock), 0, s, x,
+                       K, lp, d_idx, d_par, n_defer, evals, status);
+  } else {
+    // direct family: only exact-path records, one lane each
+    const int64_t nl = (n + 63) / 64;
+    const int64_t g = nl < 2048 ? nl : 2048;
     hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
                        d_idx, d_par, n_defer, evals, status);
-  else if (stk == 1)
-    hipLaunchKernelGGL((node_slow_kernel<MODE, 1, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
-                       d_idx, d_par, n_defer, evals, status);
-  else
-    hipLaunchKernelGGL((node_slow_kernel<MODE, 2, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
-                       d_idx, d_par, n_defer, evals, status);
+  }
 }
 
 void launch_multi_fast(int mode, const double* x, int64_t n, const double* const* arr,

@@ -185,6 +185,7 @@ class HDDM:
         self.n_trials = rt.size
         self.likelihood_calls = 0
         self.likelihood_seconds = 0.0
+        self.call_stats = {}  # updated parameter -> [calls, seconds]
         self._init_values()
 
     # -- state ---------------------------------------------------------------
@@ -230,8 +231,13 @@ class HDDM:
     def node_logp(self, over=None):
         t0 = time.perf_counter()
         out = self.dataset.wiener_like_nodes(self.node_table(over), **self.wp)
-        self.likelihood_seconds += time.perf_counter() - t0
+        dt = time.perf_counter() - t0
+        self.likelihood_seconds += dt
         self.likelihood_calls += 1
+        key = ",".join(sorted(over)) if over else "-"
+        st = self.call_stats.setdefault(key, [0, 0.0])
+        st[0] += 1
+        st[1] += dt
         return out
 
     def subj_prior(self, fam, x):

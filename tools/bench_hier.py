@@ -44,6 +44,7 @@ def main():
              seed=1)
     m.sample(a.burn, progress=a.progress or None)  # burn-in (untimed)
     c0, s0 = m.likelihood_calls, m.likelihood_seconds
+    m.call_stats = {}
     t0 = time.perf_counter()
     m.sample(a.iters, progress=a.progress or None)
     el = time.perf_counter() - t0
@@ -73,6 +74,8 @@ def main():
                                  np.asarray(truth[f] if f != "v" else truth["v"]["c0"]))[0, 1])
             for f in ("a", "t", "v")},
         "burn": a.burn,
+        "likelihood_calls_by_update": {k: {"calls": c, "us_per_call": t / c * 1e6}
+                                       for k, (c, t) in sorted(m.call_stats.items())},
     }
     # the reference's CPU cost of the same node evaluations: the C restatement
     # of wiener_like (oracle/wfpt_oracle.c, calibrated 1.0x against the
@@ -90,6 +93,28 @@ def main():
         "likelihood_s_per_sweep": per_node * node_evals / a.iters,
         "note": "C restatement of the reference's wiener_like per node x the node evaluations "
                 "of one sweep; excludes PyMC/kabuki overhead (not runnable offline)"}
+    # device view of the node likelihood at the chain's final state: kernel
+    # time per batched call (HIP events around the per-node kernels) and
+    # pdf_sv evaluations per trial, for one slice update of each kind
+    from hddm_amd import _lib
+    ctx = _lib.context()
+    dev = {}
+    for kind in ("v", "a", "t", "sv", "sz", "st"):
+        if kind in ("sv", "sz", "st") and kind not in m.include:
+            continue
+        over = {kind: m.subj[kind] if kind in m.FAMILIES else m.inter[kind]}
+        ctx.profile(ctx.PROF_EVENTS)
+        ctx.profile_read(reset=True)
+        for _ in range(20):
+            m.node_logp(over)
+        k_ms, nl, _ = ctx.profile_read(reset=True)
+        ctx.profile(ctx.PROF_EVALS)
+        m.node_logp(over)
+        _, _, ne = ctx.profile_read(reset=True)
+        ctx.profile(0)
+        dev[kind] = {"kernel_us": k_ms / max(nl, 1) * 1e3, "evals_per_trial": ne / m.n_trials}
+    out["device_per_call"] = dev
+    out["state"] = {k: float(v) for k, v in m.inter.items()}
     line = json.dumps(out)
     print(line, flush=True)
     if a.json:
