@@ -314,7 +314,7 @@ bool engine_family(const wfpt::Params& P, const wfpt::Knobs& K) {
 // completion word to `out` (mapped host memory or device).
 int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
             const wfpt::Knobs& K, double* out, int part = wfpt::kPassAll,
-            const wfpt_ds* d = nullptr) {
+            const wfpt_ds* d = nullptr, double* mirror = nullptr) {
   const int64_t nb = wfpt::partials_for(n, P, K);
   HIP_TRY(c->part.reserve(std::max<int64_t>(nb, 1)));
   HIP_TRY(c->zero.reserve(std::max<int64_t>(nb, 1)));
@@ -338,7 +338,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   HIP_TRY(hipGetLastError());
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? 1 : 0,
                         c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
-                        eng ? d->hcount + d->parity : nullptr, c->tree_any);
+                        eng ? d->hcount + d->parity : nullptr, c->tree_any, mirror);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -970,13 +970,26 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   HIP_TRY(c->res.reserve(6));
-  // no host round trip before the exchange: the lean prediction runs the
-  // redo pass unconditionally (an empty one exits per wave on its flag)
   const bool eng = engine_family(P, K);
   const bool lean = eng && c->lean && d->no_tree && !c->count;
-  if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p,
-                       wfpt::kPassAll | (lean ? wfpt::kPassLean | wfpt::kPassRedo : 0), d))
+  if (lean) {
+    // the lean prediction settles the local sum before the exchange: level-0
+    // pass + finalize (result to the mapped slot and to the device buffer the
+    // exchange reads); a misprediction adds the redo + fold passes and a second
+    // finalize after one host round trip (an unconditional redo launch would
+    // dispatch one wave per chunk: ~48k blocks at 12.5M trials)
+    if (int rc = run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d,
+                         c->res.p))
+      return rc;
+    if (int rc = wait_result(c, c->mres)) return rc;
+    if (res_deferred(c->mres)) {
+      if (int rc = run_sum(c, d->x, d->n, P, K, c->mres_dev,
+                           wfpt::kPassDeferred | wfpt::kPassRedo, d, c->res.p))
+        return rc;
+    }
+  } else if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p, wfpt::kPassAll, d)) {
     return rc;
+  }
   // {sum, zeros, encoded errors} of every rank summed: any zero trial or
   // failure anywhere reaches every rank (the error encoding keeps depth and
   // budget failures apart under the sum, wfpt_internal.h: kBudgetUnit)

@@ -85,12 +85,13 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
 // kResDeferred (defer_bits: some chunk's zero word carries kZeroDefer) |
 // kResTree (*tree_any; then *tree_any = 0)}, out[5] = *split_rd (the heavy chunks the call
 // recorded, or 0; then *split_rs = 0), then out[4] = seq (a 64-bit word) once
-// they are visible; resets *status to 0.
+// they are visible; resets *status to 0. mirror (optional, device memory):
+// out[0..3] and out[5] written there too.
 constexpr int kResDeferred = 1, kResTree = 2;
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
                      const int* split_rd = nullptr, int* split_rs = nullptr,
-                     int* tree_any = nullptr);
+                     int* tree_any = nullptr, double* mirror = nullptr);
 // res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then
 // out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);

@@ -987,7 +987,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
                                                         int* status, double* out,
                                                         unsigned long long seq,
                                                         const int* split_rd, int* split_rs,
-                                                        int* tree_any) {
+                                                        int* tree_any, double* mirror) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
   __shared__ int sd[16];
@@ -1044,6 +1044,13 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     // heavy chunks recorded for the next call (Split)
     out[5] = split_rd ? (double)*split_rd : 0.0;
     if (split_rs) *split_rs = 0;
+    if (mirror) {  // device copy of the result (the RCCL exchange reads it)
+      mirror[0] = out[0];
+      mirror[1] = out[1];
+      mirror[2] = out[2];
+      mirror[3] = out[3];
+      mirror[5] = out[5];
+    }
     __threadfence_system();
     // completion word, written after the results are visible: the host may
     // poll it instead of waiting on the stream
@@ -1498,9 +1505,9 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
-                     const int* split_rd, int* split_rs, int* tree_any) {
+                     const int* split_rd, int* split_rs, int* tree_any, double* mirror) {
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, defer_bits,
-                     status, out, seq, split_rd, split_rs, tree_any);
+                     status, out, seq, split_rd, split_rs, tree_any, mirror);
 }
 
 template <int MODE, bool COUNT>
