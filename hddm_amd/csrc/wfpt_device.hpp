@@ -1070,6 +1070,10 @@ __device__ inline void tree_root(const Trial& tr, const Params& P, double& lb, d
 //           k * kTreeW / 4); f[] = the root interval's values at lb, d, c, e, ub;
 //   kExact: the value hinges on last-bit rounding (recomputed exactly).
 template <int MODE>
+__device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
+                                 double& p, double (&f)[5], long long& ne, unsigned& pend);
+
+template <int MODE>
 __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, double& p,
                                   double (&f)[5], long long& ne, int& flags, unsigned& pend) {
   const Trial tr = trial_setup(x0, P);
@@ -1084,94 +1088,14 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
     if (flags & kFlagExact) return kExact;
     return (p > kExactBelow || x - t <= 0) ? kFinal : kExact;
   }
-  double lb, ub;
-  tree_root<MODE>(tr, P, lb, ub);
-  const double iw = 1.0 / (ub - lb);
-  if (MODE == kAdaptZ) {
-    const ZGrid G = zgrid_setup(lb, ub, v, sv, a);
-    const TNode T = tnode_setup(x - t, v, sv, a, err);
-    if (T.amb) return kExact;
-    tnode_pdf_sv_grid5(T, G, v, sv, a, f);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
-    ne += 5;
-  } else {
-    // t outer: kAdaptT (one evaluation per t node) or kAdaptTZ (a z integral
-    // per t node)
-    const double c = (ub + lb) / 2.;
-    const double d = (lb + c) / 2., e = (c + ub) / 2.;
-    const double lbz = z - tr.sz / 2., ubz = z + tr.sz / 2.;
-    const double iZz = (MODE == kAdaptTZ) ? 1.0 / (ubz - lbz) : 0.0;
-    {
-      ZGrid G;
-      if (MODE == kAdaptTZ) G = zgrid_setup(lbz, ubz, v, sv, a);
-      // large-time factor q = exp(-pi^2 (x - tc) / (2 a^2)) over the t grid:
-      // q(lb + j (ub - lb) / 4) = q(lb) R^j, R = exp(pi^2 (ub - lb) / (8 a^2))
-      // (values only; direct exps where the products leave the safe range)
-      double qn[5] = {-1.0, -1.0, -1.0, -1.0, -1.0};
-      {
-        const double a2 = a * a;
-        const double q0 = exp((-kPi2 * ((x - lb) / a2)) / 2.0);
-        const double R = exp((kPi2 * (ub - lb)) / (8.0 * a2));
-        if (q0 > 1e-280 && R < 1e10 && x - lb > 0) {
-          const double R2 = R * R;
-          qn[0] = q0;
-          qn[1] = q0 * R;
-          qn[2] = q0 * R2;
-          qn[3] = q0 * (R2 * R);
-          qn[4] = q0 * (R2 * R2);
-        }
-      }
-      // Shared series decision: ks(tt) increases and kl(tt) decreases with tt
-      // (pdf.pxi:36-47; ks only while its log argument stays below e^-1/2,
-      // hence the 0.5 test at the largest tt), so when the outermost t nodes
-      // (largest / smallest tt) take the same branch and K with both fp32
-      // decisions clear of every threshold, all 5 nodes do. Otherwise each
-      // node decides itself.
-      Decision D0{0, 0, 0}, D4{0, 0, 0};
-      bool ok0 = false, ok4 = false, shared = false;
-      if (x - ub > 0) {
-        const double a2 = a * a;
-        float args0, args4;
-        ok0 = decide32((x - lb) / a2, err, D0, args0);
-        ok4 = decide32((x - ub) / a2, err, D4, args4);
-        shared = ok0 && ok4 && args0 < 0.5f && D0.small == D4.small && D0.K == D4.K;
-      }
-#pragma unroll 1
-      for (int j = 0; j < 5; ++j) {
-        const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
-        const double qh = j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
-        const bool known = j == 0 ? ok0 : (j == 4 ? ok4 : shared);
-        const TNode T = tnode_setup(x - tc, v, sv, a, err, qh, known, j == 4 ? D4 : D0);
-        if (T.amb) return kExact;
-        double y;
-        if (MODE == kAdaptTZ) {
-          bool rep;
-          y = inner_root(T, G, iZz, v, sv, a, K, flags, ne, rep) * iw;
-          if (flags & kFlagExact) return kExact;
-          if (rep) pend |= 1u << (j * (kTreeW / 4));
-        } else {
-          ne += 1;
-          y = tnode_pdf_sv(T, z, v, sv, a) * iw;
-        }
-        if (j == 0) f[0] = y;
-        else if (j == 1) f[1] = y;
-        else if (j == 2) f[2] = y;
-        else if (j == 3) f[3] = y;
-        else f[4] = y;
-      }
-    }
-  }
-  if (pend) return kTree;  // root test after the z-integral repairs
-  const Simp s = simp5(ub - lb, f[0], f[1], f[2], f[3], f[4]);
-  const int bottom = (MODE == kAdaptZ) ? K.n_sz : K.n_st;
-  const bool refine = simpson_refine(s.S, s.S2, K.simps_err, bottom, flags);
-  if (flags & kFlagExact) return kExact;
-  if (refine) return kTree;
-  p = s.S2 + (s.S2 - s.S) / 15;
-  // structural zero: every evaluation point has x - t_node <= 0 (x == lb for t trees)
-  const bool structural = (MODE == kAdaptZ) ? x - t <= 0 : x - lb <= 0;
-  return (p > kExactBelow || structural) ? kFinal : kExact;
+  // adaptive families: the engine's level 0 (eng_level0, defined below) on
+  // this trial's own root z grid
+  ZGrid G{};
+  if (MODE == kAdaptZ || MODE == kAdaptTZ)
+    G = zgrid_setup(z - tr.sz / 2., z + tr.sz / 2., v, sv, a);
+  (void)t;
+  (void)x;
+  return eng_level0<MODE>(x0, P, K, G, p, f, ne, pend);
 }
 
 // The engine's level 0 (kAdaptT / kAdaptTZ): the same operations as
