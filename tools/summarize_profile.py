@@ -41,14 +41,19 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="void wfpt::lean_kernel<3, false, 0>")
     ap.add_argument("--trials", type=int, default=1_000_000)
+    ap.add_argument("--prof-dir", default=PROF, help="tools/gpu_profile*.sh output directory")
+    ap.add_argument("--name", default="pmc_summary", help="summary file name under profiles/<tag>/")
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="do not write profiles/traffic.json (secondary kernels)")
     a = ap.parse_args()
+    prof = a.prof_dir
     out_dir = os.path.join(ROOT, "profiles", a.tag)
     os.makedirs(out_dir, exist_ok=True)
-    stats = list(csv.DictReader(open(os.path.join(PROF, "trace", "trace_kernel_stats.csv"))))
+    stats = list(csv.DictReader(open(os.path.join(prof, "trace", "trace_kernel_stats.csv"))))
     k_ns = next(float(r["AverageNs"]) for r in stats if r["Name"].startswith(a.kernel))
     res, meta = {}, {}
     for grp in ("fetch", "write", "sq", "f64"):
-        p = os.path.join(PROF, grp, f"{grp}_counter_collection.csv")
+        p = os.path.join(prof, grp, f"{grp}_counter_collection.csv")
         if os.path.exists(p):
             r, m = per_launch(p, a.kernel)
             res.update(r)
@@ -75,17 +80,19 @@ def main():
         "valu_issue_utilisation": simd_cycles / (t * clk) if clk else None,
         "valu_busy_wave": res.get("SQ_ACTIVE_INST_VALU", 0) / max(res.get("SQ_WAVE_CYCLES", 1), 1),
     }
-    with open(os.path.join(out_dir, "pmc_summary.json"), "w") as fh:
-        json.dump(summary, fh, indent=1)
-    shutil.copy(os.path.join(PROF, "trace", "trace_kernel_stats.csv"),
-                os.path.join(out_dir, "kernel_stats.csv"))
+    shutil.copy(os.path.join(prof, "trace", "trace_kernel_stats.csv"),
+                os.path.join(out_dir, "kernel_stats.csv" if a.name == "pmc_summary"
+                             else a.name + "_kernel_stats.csv"))
     # the digest of the library the GPU run profiled (tools/gpu_profile.sh
     # records it next to the counters), not whatever is built here now
-    with open(os.path.join(PROF, "src_sha1.txt")) as fh:
+    with open(os.path.join(prof, "src_sha1.txt")) as fh:
         sha = fh.read().strip()
     summary["src_sha1"] = sha
-    with open(os.path.join(out_dir, "pmc_summary.json"), "w") as fh:
+    with open(os.path.join(out_dir, a.name + ".json"), "w") as fh:
         json.dump(summary, fh, indent=1)
+    if a.no_traffic:
+        print(json.dumps(summary, indent=1))
+        return
     with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as fh:
         json.dump({"src_sha1": sha, "source": f"profiles/{a.tag}/pmc_summary.json", "kernel": a.kernel,
                    "n_trials": a.trials, "hbm_bytes_per_launch": fetch_b + write_b,
