@@ -65,17 +65,34 @@ def _patch(inst, key, target, ours, names):
     return target
 
 
-def install(wfpt_module=None, cdfdif_module=None):
+def install(wfpt_module=None, cdfdif_module=None, likelihoods_module=None):
     """Route HDDM's likelihood and CDF calls to libwfpt_amd.so.
 
     `wfpt_module` / `cdfdif_module` default to the already-imported (or
     importable) reference extensions `wfpt` and `cdfdif_wrapper`; when one is
     absent, the MI355X module is registered under its name instead. Call before
     or after `import hddm`: attributes are looked up per call. Returns an
-    Installation whose `uninstall()` restores the previous state."""
+    Installation whose `uninstall()` restores the previous state.
+
+    If `hddm.likelihoods` is already imported (or given), its
+    `generate_wfpt_stochastic_class` (called by HDDM models at construction,
+    hddm/models/base.py:727,738) and `Wfpt` are rebound too, to this package's
+    factory: the same PyMC class (kabuki's stochastic_from_dist with pdf, cdf,
+    cdf_vec, random and the quantile methods), whose logp keeps each node's
+    RTs resident on the GPU instead of uploading them per call. HDDM is never
+    imported here."""
     from . import cdfdif_wrapper as amd_cdf
+    from . import likelihoods as amd_lk
     from . import wfpt as amd_wfpt
     inst = Installation()
     _patch(inst, "wfpt", _find("wfpt", wfpt_module), amd_wfpt, HOT_PATH)
     _patch(inst, "cdfdif_wrapper", _find("cdfdif_wrapper", cdfdif_module), amd_cdf, CDF_PATH)
+    lk = likelihoods_module if likelihoods_module is not None else sys.modules.get("hddm.likelihoods")
+    if lk is not None:
+        inst._attrs.append((lk, "generate_wfpt_stochastic_class",
+                            getattr(lk, "generate_wfpt_stochastic_class", _MISSING)))
+        lk.generate_wfpt_stochastic_class = amd_lk.generate_wfpt_stochastic_class
+        if hasattr(lk, "Wfpt"):
+            inst._attrs.append((lk, "Wfpt", lk.Wfpt))
+            lk.Wfpt = amd_lk.generate_wfpt_stochastic_class()
     return inst

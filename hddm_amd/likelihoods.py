@@ -218,4 +218,14 @@ def generate_wfpt_stochastic_class(wiener_params=None, sampling_method="cdf",
     wfpt_cls.pdf = pdf
     wfpt_cls.cdf = cdf
     wfpt_cls.random = random
+    # likelihoods.py:98,103: cdf_vec over the reference's gen_cdf_using_pdf (not
+    # on the accelerated path) and the quantile methods, when HDDM is loaded
+    try:
+        import hddm
+        wp = wfpt_like.wiener_params
+        wfpt_cls.cdf_vec = lambda self: hddm.wfpt.gen_cdf_using_pdf(
+            time=cdf_range[1], **dict(list(self.parents.items()) + list(wp.items())))
+        hddm.likelihoods.add_quantiles_functions_to_pymc_class(wfpt_cls)
+    except (ImportError, AttributeError):
+        pass
     return wfpt_cls

@@ -85,8 +85,14 @@ def test_install_patches_hot_path_only():
         setattr(ref, n, lambda *a, _n=n: _n)
     cdf = types.ModuleType("cdfdif_wrapper")
     cdf.dmat_cdf_array = lambda *a: "ref"
+    lk = types.ModuleType("hddm.likelihoods")
+    lk.generate_wfpt_stochastic_class = lambda *a, **k: "ref-class"
+    lk.Wfpt = "ref-Wfpt"
     held_by_rl = ref                      # `import wfpt` in hddm/models/hddm_rl.py
-    inst = integration.install(ref, cdf)
+    from hddm_amd import likelihoods as amd_lk
+    inst = integration.install(ref, cdf, lk)
+    assert lk.generate_wfpt_stochastic_class is amd_lk.generate_wfpt_stochastic_class
+    assert lk.Wfpt != "ref-Wfpt"
     for n in integration.HOT_PATH:
         assert getattr(held_by_rl, n) is getattr(amd, n)
     assert held_by_rl.wiener_like_rl() == "wiener_like_rl"
@@ -94,6 +100,7 @@ def test_install_patches_hot_path_only():
     assert cdf.dmat_cdf_array is amd_cdf.dmat_cdf_array
     inst.uninstall()
     assert ref.wiener_like() == "wiener_like" and cdf.dmat_cdf_array() == "ref"
+    assert lk.generate_wfpt_stochastic_class() == "ref-class" and lk.Wfpt == "ref-Wfpt"
     # no reference extension importable here: ours under the module names
     had = {k: sys.modules.get(k) for k in ("wfpt", "cdfdif_wrapper")}
     inst = integration.install()
