@@ -966,9 +966,18 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 #pragma unroll
     for (int i = 0; i < 5; ++i) ex[i] = exp(cexp[i]);
   }
+  // the common case: every series value positive and every product finite;
+  // the rare fix-ups below run only on lanes that need one (same values)
+  bool clean = true;
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
-    double r2 = (p[i] * ex[i]) * T.sc;
+    out[i] = (p[i] * ex[i]) * T.sc;
+    clean = clean & (p[i] > 0) & !__builtin_isinf(out[i]);
+  }
+  if (__builtin_expect(clean, 1)) return;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    double r2 = out[i];
     if (sv != 0 && p[i] < 0) r2 = __builtin_nan("");  // log(p < 0) in the reference
     // exp(log 0 + c) = 0 even if e^c = inf; 0 * sc keeps the reference's
     // 0 / (a*a) = NaN at a == 0
