@@ -843,6 +843,38 @@ __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, d
   return G;
 }
 
+// exp(x) for the grid evaluation's finite arguments (series terms and drift
+// factors, values only): x = k ln2 + r, |r| <= ln2/2, a degree-11 polynomial
+// (Chebyshev-node fit: max relative error 1.2e-16 in double Horner steps),
+// then ldexp, which also saturates to inf / 0 / subnormals for |x| > 709. No
+// special-case selects (OCML's exp carries them for inf / NaN arguments,
+// which these call sites never pass). WFPT_FAST_EXP=0 restores OCML's exp.
+#ifndef WFPT_FAST_EXP
+#define WFPT_FAST_EXP 1
+#endif
+__device__ inline double exp_val(double x) {
+#if WFPT_FAST_EXP
+  const double k = rint(x * 1.4426950408889634);
+  double r = fma(-k, 6.9314718055994529e-01, x);
+  r = fma(-k, 2.3190468138462996e-17, r);
+  double p = 2.5110037605963777e-08;
+  p = fma(p, r, 2.763263963904103e-07);
+  p = fma(p, r, 2.755724091857897e-06);
+  p = fma(p, r, 2.4801485482328494e-05);
+  p = fma(p, r, 1.9841269890047113e-04);
+  p = fma(p, r, 1.3888888952314775e-03);
+  p = fma(p, r, 8.333333333319601e-03);
+  p = fma(p, r, 4.16666666664881e-02);
+  p = fma(p, r, 1.666666666666668e-01);
+  p = fma(p, r, 5.000000000000019e-01);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)k);
+#else
+  return exp(x);
+#endif
+}
+
 // pdf_sv at the 5 root-level z nodes of one t node (the values of
 // tnode_pdf_sv at each node to a few ulp):
 //   * small-t series: the exponents (g_j + 2k)^2 m are quadratic in j on the
@@ -879,11 +911,11 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
       if (ek[0] > -600.0 && ek[4] > -600.0) {  // ek <= 0 and convex in j: ends are the minima
         const double d1 = ek[1] - ek[0];
         if (!have_q) {
-          qq = exp((ek[2] - ek[1]) - d1);
+          qq = exp_val((ek[2] - ek[1]) - d1);
           have_q = true;
         }
-        double E = exp(ek[0]);
-        double R = exp(d1);
+        double E = exp_val(ek[0]);
+        double R = exp_val(d1);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
           p[i] = madd(wk[i], E, p[i]);
@@ -892,7 +924,7 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) p[i] = madd(wk[i], exp(ek[i]), p[i]);
+        for (int i = 0; i < 5; ++i) p[i] = madd(wk[i], exp_val(ek[i]), p[i]);
       }
     }
 #pragma unroll
@@ -954,9 +986,9 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     // c_j = c0 + j d1 + j(j-1)/2 d2  ->  E_j = E_{j-1} * R * Q^(j-1)
     const double d1 = cexp[1] - cexp[0];
     const double d2 = (cexp[2] - cexp[1]) - d1;
-    ex[0] = exp(cexp[0]);
-    double rr = exp(d1);
-    const double qd = exp(d2);
+    ex[0] = exp_val(cexp[0]);
+    double rr = exp_val(d1);
+    const double qd = exp_val(d2);
 #pragma unroll
     for (int j = 1; j < 5; ++j) {
       ex[j] = ex[j - 1] * rr;
@@ -964,7 +996,7 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 5; ++i) ex[i] = exp(cexp[i]);
+    for (int i = 0; i < 5; ++i) ex[i] = exp_val(cexp[i]);
   }
   // the common case: every series value positive and every product finite;
   // the rare fix-ups below run only on lanes that need one (same values)
