@@ -165,24 +165,34 @@ struct Decision {
 // 1e-5 (relative) of flipping or an fp32 argument is out of range. args_out:
 // the small-time log argument 2 sqrt(2 pi tt) err (for the monotonicity test
 // of shared decisions).
+// Hardware fp32 log / sqrt / reciprocal for the estimate (v_log_f32,
+// v_sqrt_f32, v_rcp_f32: ~1 ulp on the normal range these arguments stay in,
+// i.e. relative errors ~1e-7 in kl / ks, 100x inside the 1e-5 guard band).
+__device__ inline float log32(float x) { return __builtin_amdgcn_logf(x) * 0.69314718055994531f; }
+__device__ inline float sqrt32(float x) { return __builtin_amdgcn_sqrtf(x); }
+__device__ inline float rcp32(float x) { return __builtin_amdgcn_rcpf(x); }
+
 __device__ inline bool decide32(double tt, double err, Decision& D, float& args_out) {
   args_out = 2.0f;
   if (!(tt > 1e-30 && tt < 1e30 && err > 1e-30 && err < 1e30)) return false;
   const float ttf = (float)tt, errf = (float)err;
-  const float sqtf = sqrtf(ttf);
-  const float ipsf = 1.0f / ((float)kPi * sqtf);
+  const float sqtf = sqrt32(ttf);
+  const float ipsf = rcp32((float)kPi * sqtf);
   const float argl = ((float)kPi * ttf) * errf;
-  const float args = (2.0f * sqrtf((2.0f * (float)kPi) * ttf)) * errf;
+  const float args = (2.0f * sqrt32((2.0f * (float)kPi) * ttf)) * errf;
   args_out = args;
   const bool use_l = argl < 1.0f;
   const bool use_s = args < 1.0f;
   const float tol = 1e-5f;
-  // |dL| <~ 2e-7 from fp32 rounding + logf; the relative error it induces in
-  // kl/ks is <= |dL| / (2|L|), so |L| >= 0.1 keeps it <= 1e-6 (10x inside tol).
-  const float Ll = use_l ? logf(argl) : -1.0f;
-  const float Ls = use_s ? logf(args) : -1.0f;
-  float klf = use_l ? sqrtf((-2.0f * Ll) / ((float)kPi2 * ttf)) : ipsf;
-  float ksf = use_s ? 2.0f + sqrtf((-2.0f * ttf) * Ls) : 2.0f;
+  // |dL| <~ 1e-7 |L| from fp32 rounding + the hardware log; the relative error
+  // it induces in kl/ks is <= |dL| / (2|L|) ~ 1e-7, 100x inside tol (and |L| >=
+  // 0.1 is still required below, as for the correctly rounded logf).
+  const bool rng = (use_l && !(argl > 1e-30f)) || (use_s && !(args > 1e-30f));
+  if (rng) return false;
+  const float Ll = use_l ? log32(argl) : -1.0f;
+  const float Ls = use_s ? log32(args) : -1.0f;
+  float klf = use_l ? sqrt32((-2.0f * Ll) * rcp32((float)kPi2 * ttf)) : ipsf;
+  float ksf = use_s ? 2.0f + sqrt32((-2.0f * ttf) * Ls) : 2.0f;
   const float b2 = sqtf + 1.0f;
   const bool amb_t = fabsf(argl - 1.0f) <= tol || fabsf(args - 1.0f) <= tol;
   const bool amb_l = use_l && fabsf(klf - ipsf) <= tol * klf;
@@ -192,8 +202,7 @@ __device__ inline bool decide32(double tt, double err, Decision& D, float& args_
   const float kk = (ksf < klf) ? ksf : klf;
   const bool amb_b = fabsf(ksf - klf) <= tol * klf;
   const bool amb_k = fabsf(kk - rintf(kk)) <= tol * kk;
-  const bool rng = (use_l && !(argl > 1e-30f)) || (use_s && !(args > 1e-30f));
-  if (rng || Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k) return false;
+  if (Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k) return false;
   D.small = ksf < klf;
   D.K = (int)ceilf(kk);
   D.amb = 0;
