@@ -184,7 +184,7 @@ def main():
     ds = wfpt.Dataset(x, device=local)
     if world > 1:
         from hddm_amd import dist as hdist
-        hdist.init_comm(ctx, rank, world, pg)
+        hdist.init_comm(ctx, rank, world)  # the library's TCP rendezvous (no torch)
         step = lambda: ds.wiener_like_allreduce(*args_tuple(), *knobs_tuple())
     else:
         step = lambda: ds.wiener_like(*args_tuple(), *knobs_tuple())

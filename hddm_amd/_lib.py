@@ -82,10 +82,23 @@ wfpt_wiener_like_multi = _sig("wfpt_wiener_like_multi", _I,
                               [_VP, _PD, _I64, ctypes.POINTER(_PD), _PD, _PK, _D, _PD])
 wfpt_wiener_like_multi_resident = _sig("wfpt_wiener_like_multi_resident", _I,
                                        [_VP, _VP, ctypes.POINTER(_PD), _PD, _PK, _D, _PD])
+wfpt_wiener_like_nodes_ex = _sig("wfpt_wiener_like_nodes_ex", _I, [_VP, _VP, _PP, _PK, _PD, _PD])
+wfpt_wiener_like_multi_ex = _sig("wfpt_wiener_like_multi_ex", _I,
+                                 [_VP, _PD, _I64, ctypes.POINTER(_PD), _PD, _PK, _D, _PD, _PD])
+wfpt_wiener_like_multi_resident_ex = _sig("wfpt_wiener_like_multi_resident_ex", _I,
+                                          [_VP, _VP, ctypes.POINTER(_PD), _PD, _PK, _D, _PD, _PD])
 wfpt_dmat_cdf_array = _sig("wfpt_dmat_cdf_array", _I, [_VP, _PD, _I64, _PP, _D, _PD])
 wfpt_comm_unique_id = _sig("wfpt_comm_unique_id", _I, [ctypes.c_char_p])
 wfpt_comm_init = _sig("wfpt_comm_init", _I, [_VP, _I, _I, ctypes.c_char_p])
 wfpt_wiener_like_allreduce = _sig("wfpt_wiener_like_allreduce", _I, [_VP, _VP, _PP, _PK, _PD])
+wfpt_comm_exchange_id = _sig("wfpt_comm_exchange_id", _I,
+                             [_I, _I, ctypes.c_char_p, _I, _I, ctypes.c_char_p])
+wfpt_comm_init_tcp = _sig("wfpt_comm_init_tcp", _I, [_VP, _I, _I, ctypes.c_char_p, _I, _I])
+wfpt_comm_init_all = _sig("wfpt_comm_init_all", _I, [ctypes.POINTER(_VP), _I])
+wfpt_wiener_like_allreduce_group = _sig("wfpt_wiener_like_allreduce_group", _I,
+                                        [ctypes.POINTER(_VP), ctypes.POINTER(_VP), _I, _PP, _PK,
+                                         _PD])
+wfpt_result_poison = _sig("wfpt_result_poison", _I, [_PD])
 wfpt_profile_enable = _sig("wfpt_profile_enable", _I, [_VP, _I])
 wfpt_profile_read = _sig("wfpt_profile_read", _I,
                          [_VP, _PD, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I])
@@ -104,12 +117,23 @@ EXPORTED = [
     "wfpt_wiener_like_multi", "wfpt_dmat_cdf_array", "wfpt_comm_unique_id", "wfpt_comm_init",
     "wfpt_wiener_like_allreduce", "wfpt_profile_enable", "wfpt_profile_read", "wfpt_synchronize",
     "wfpt_decode_result", "wfpt_profile_lists", "wfpt_debug_waves", "wfpt_dataset_create_ex",
-    "wfpt_wiener_like_multi_resident",
+    "wfpt_wiener_like_multi_resident", "wfpt_comm_exchange_id", "wfpt_comm_init_tcp",
+    "wfpt_comm_init_all", "wfpt_wiener_like_allreduce_group", "wfpt_result_poison",
+    "wfpt_wiener_like_nodes_ex", "wfpt_wiener_like_multi_ex", "wfpt_wiener_like_multi_resident_ex",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)
 DEPTH_ERROR = 1.0
 BUDGET_ERROR = 1048576.0
+PEER_FAILED = 1099511627776.0  # 2^40: a rank that failed before the exchange
+
+
+def poisoned_result():
+    """The triple a rank that failed before the exchange contributes
+    (wfpt_result_poison)."""
+    r = (ctypes.c_double * 3)()
+    check(wfpt_result_poison(r))
+    return [r[0], r[1], r[2]]
 
 
 def decode_result(triple):
@@ -120,6 +144,11 @@ def decode_result(triple):
     return out.value
 
 
+class CommError(RuntimeError):
+    """A multi-GPU exchange failed (WFPT_ERR_COMM), e.g. another rank's local
+    pass failed before the all-reduce."""
+
+
 def check(rc):
     if rc != WFPT_OK:
         msg = wfpt_last_error().decode(errors="replace")
@@ -127,6 +156,8 @@ def check(rc):
             raise NotImplementedError(f"wfpt_amd: {msg}")
         if rc == 2:
             raise ValueError(f"wfpt_amd: {msg}")
+        if rc == 3:
+            raise CommError(f"wfpt_amd error {rc}: {msg}")
         raise RuntimeError(f"wfpt_amd error {rc}: {msg}")
 
 

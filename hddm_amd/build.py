@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 LIB = os.path.join(LIBDIR, "libwfpt_amd.so")
-SOURCES = ["wfpt_kernels.hip", "cdfdif_kernels.hip", "wfpt_capi.cpp"]
+SOURCES = ["wfpt_kernels.hip", "cdfdif_kernels.hip", "wfpt_capi.cpp", "wfpt_rendezvous.cpp"]
 DEPS = SOURCES + ["wfpt_device.hpp", "wfpt_internal.h", "wfpt_crlibm.hpp", "wfpt_exact.hpp"]
 ARCH = os.environ.get("WFPT_OFFLOAD_ARCH", "gfx950")
 
@@ -79,7 +79,7 @@ def build(force=False, verbose=False, defines=(), out=None):
         objs.append(obj)
     tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
-           "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+           "-L/opt/rocm/lib", "-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

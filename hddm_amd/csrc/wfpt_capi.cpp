@@ -9,6 +9,7 @@
 // releases the GIL around every call.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <atomic>
@@ -31,6 +32,30 @@ static int fail(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
+// the last-error slot for wfpt_rendezvous.cpp
+int wfpt_rdv_fail(int code, const std::string& msg) { return fail(code, msg); }
+
+// roctx range around each C-ABI entry point (rocprofv3 --marker-trace shows
+// the host side of a call next to its kernels); WFPT_ROCTX=0 turns them off.
+static bool roctx_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("WFPT_ROCTX");
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  return on;
+}
+namespace {
+struct RoctxRange {
+  bool on;
+  explicit RoctxRange(const char* name) : on(roctx_on()) {
+    if (on) roctxRangePushA(name);
+  }
+  ~RoctxRange() {
+    if (on) roctxRangePop();
+  }
+};
+}  // namespace
+#define WFPT_RANGE(name) RoctxRange wfpt_range_(name)
 
 #define HIP_TRY(expr)                                                                 \
   do {                                                                                \
@@ -168,6 +193,9 @@ struct wfpt_ds {
   int* hzn = nullptr;
   mutable int nsplit = 0;  // chunks the next call splits
   mutable int parity = 0;
+  // node datasets: the caller's index of each stored trial (per-trial
+  // outputs of wfpt_wiener_like_nodes_ex are returned in the caller's order)
+  std::vector<int64_t> perm;
 };
 
 namespace {
@@ -258,17 +286,24 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
 // #depth errors + kBudgetUnit * #budget errors (summed over ranks).
 int check_status_value(double enc) {
   if (enc == 0) return WFPT_OK;
+  const double peers = std::floor(enc / wfpt::kPeerFailUnit);
+  enc -= peers * wfpt::kPeerFailUnit;
   const double budget = std::floor(enc / wfpt::kBudgetUnit);
   const double depth = enc - budget * wfpt::kBudgetUnit;
   std::string msg;
-  if (depth > 0)
-    msg = "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
-          std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)";
+  if (peers > 0)
+    msg = std::to_string((long long)peers) +
+          " rank(s) failed before the likelihood exchange (their own call returned the error)";
+  if (depth > 0) {
+    if (!msg.empty()) msg += "; ";
+    msg += "adaptive Simpson refinement deeper than WFPT_MAX_DEPTH=" +
+           std::to_string(WFPT_MAX_DEPTH) + " levels (lower n_st/n_sz or raise simps_err)";
+  }
   if (budget > 0) {
     if (!msg.empty()) msg += "; ";
     msg += "a trial exceeded WFPT_EVAL_BUDGET pdf_sv evaluations (raise simps_err)";
   }
-  return fail(WFPT_ERR_UNSUPPORTED, msg);
+  return fail((depth > 0 || budget > 0) ? WFPT_ERR_UNSUPPORTED : WFPT_ERR_COMM, msg);
 }
 
 // The dataset's heavy-chunk state for one engine call (null: no split, no
@@ -475,6 +510,14 @@ extern "C" {
 
 const char* wfpt_last_error(void) { return g_last_error.c_str(); }
 
+int wfpt_result_poison(double r[3]) {
+  if (!r) return fail(WFPT_ERR_ARG, "null pointer");
+  r[0] = 0.0;
+  r[1] = 0.0;
+  r[2] = wfpt::kPeerFailUnit;
+  return WFPT_OK;
+}
+
 int wfpt_decode_result(const double r[3], double* out) {
   if (!r || !out) return fail(WFPT_ERR_ARG, "null pointer");
   if (int rc = check_status_value(r[2])) return rc;
@@ -588,6 +631,7 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
   if (!c || !out || (n > 0 && !rt) || n < 0) return fail(WFPT_ERR_ARG, "bad dataset arguments");
   if (flags & ~WFPT_DS_INPUT_ORDER) return fail(WFPT_ERR_ARG, "unknown dataset flags");
   if (node_id && n_nodes <= 0) return fail(WFPT_ERR_ARG, "node ids need n_nodes > 0");
+  WFPT_RANGE("wfpt_dataset_create_ex");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   // host-side layout: group by node, order by |rt| inside a node so that each
@@ -613,8 +657,17 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
         std::stable_sort(idx.begin() + off[j], idx.begin() + off[j + 1],
                          [&](int64_t a, int64_t b) { return std::fabs(rt[a]) < std::fabs(rt[b]); });
   } else if (!keep_order) {
-    std::stable_sort(idx.begin(), idx.end(),
-                     [&](int64_t a, int64_t b) { return std::fabs(rt[a]) < std::fabs(rt[b]); });
+    // boundary first (x > 0 is the upper boundary, pdf.pxi:116), then |rt|:
+    // the lean pass keeps a wave's root z grid in scalar registers when the
+    // wave holds one boundary (wfpt_kernels.hip: lean_kernel)
+    // (NaN RTs last in their group: a strict weak order for any input)
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+      const bool ua = rt[a] > 0, ub = rt[b] > 0;
+      if (ua != ub) return ub;
+      const bool na = std::isnan(rt[a]), nb = std::isnan(rt[b]);
+      if (na || nb) return !na && nb;
+      return std::fabs(rt[a]) < std::fabs(rt[b]);
+    });
   }
   std::vector<double> hx(n);
   std::vector<int32_t> hn(node_id ? n : 0);
@@ -625,6 +678,7 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
   auto* d = new wfpt_ds();
   d->ctx = c;
   d->n = n;
+  if (node_id) d->perm = idx;
   d->input_order = (flags & WFPT_DS_INPUT_ORDER) != 0;
   d->n_nodes = node_id ? n_nodes : 0;
   hipError_t e = hipMalloc((void**)&d->x, std::max<int64_t>(n, 1) * sizeof(double));
@@ -693,6 +747,7 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
     *out = -INFINITY;
     return WFPT_OK;
   }
+  WFPT_RANGE("wfpt_wiener_like");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int rc = run_sum_fast(c, d, P, K, out);
@@ -710,6 +765,7 @@ int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_pa
     *out = -INFINITY;
     return WFPT_OK;
   }
+  WFPT_RANGE("wfpt_wiener_like_host");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   if (int rc = upload(c, x, n)) return rc;
@@ -724,6 +780,7 @@ int wfpt_pdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p
   const wfpt::Params P = to_params(p);
   const wfpt::Knobs K = to_knobs(k);
   if (n == 0) return WFPT_OK;
+  WFPT_RANGE("wfpt_pdf_array");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   if (int rc = upload(c, x, n)) return rc;
@@ -752,10 +809,16 @@ int wfpt_full_pdf(wfpt_ctx* c, double x, const wfpt_params* p, const wfpt_knobs*
 
 int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
                            const wfpt_knobs* k, double* out) {
+  return wfpt_wiener_like_nodes_ex(c, d, per_node, k, out, nullptr);
+}
+
+int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
+                              const wfpt_knobs* k, double* out, double* out_trial) {
   if (!c || !d || !per_node || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
   if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
   if (!d->node) return fail(WFPT_ERR_ARG, "dataset was created without node ids");
   const wfpt::Knobs K = to_knobs(k);
+  WFPT_RANGE("wfpt_wiener_like_nodes");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
@@ -798,6 +861,13 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   }
   if (int rc = finish_profile(c)) return rc;
   std::memcpy(out, c->mnode.h, m * sizeof(double));
+  if (out_trial && d->n > 0) {
+    // each trial's term (node_logp: the node's mixture, log, -inf for a zero
+    // density or p_outlier outside [0, 1]) in the caller's trial order
+    std::vector<double> h(d->n);
+    HIP_TRY(hipMemcpy(h.data(), c->lp.p, d->n * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < d->n; ++i) out_trial[d->perm[i]] = h[i];
+  }
   return WFPT_OK;
 }
 
@@ -809,7 +879,8 @@ namespace {
 // level-0 pass + deferred records (launch_multi_fast), anything else the
 // generic per-trial kernel.
 int run_multi(wfpt_ctx* c, const double* dx, int64_t n, const double* const arrays[7],
-              const double scalars[7], const wfpt::Knobs& K, double p_outlier, double* out) {
+              const double scalars[7], const wfpt::Knobs& K, double p_outlier, double* out,
+              double* out_trial) {
   int na = 0;
   for (int j = 0; j < 7; ++j) na += arrays[j] != nullptr;
   HIP_TRY(c->marr.reserve(std::max<int64_t>((int64_t)na * n, 1)));
@@ -847,8 +918,9 @@ int run_multi(wfpt_ctx* c, const double* dx, int64_t n, const double* const arra
                             c->nd_idx.p, c->nd_par.p, c->n_defer, c->part.p, c->zero.p,
                             c->count ? c->evals : nullptr, c->status, c->stream);
   } else {
+    if (out_trial && n > 0) HIP_TRY(c->lp.reserve(n));
     wfpt::launch_multi(dx, n, c->mptr.p, c->mscal.p, K, p_outlier, c->part.p, c->zero.p,
-                       c->status, c->stream);
+                       c->status, c->stream, (out_trial && n > 0) ? c->lp.p : nullptr);
   }
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
@@ -859,6 +931,10 @@ int run_multi(wfpt_ctx* c, const double* dx, int64_t n, const double* const arra
   if (int rc = check_status_value(c->mres[2])) return rc;
   if (int rc = finish_profile(c)) return rc;
   *out = c->mres[0];
+  // each trial's term log(p (1 - p_outlier) + w_outlier p_outlier), or the
+  // log prob_ub of a missing response (wfpt.pyx:261-272), in trial order
+  if (out_trial && n > 0)
+    HIP_TRY(hipMemcpy(out_trial, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost));
   return WFPT_OK;
 }
 }  // namespace
@@ -868,18 +944,33 @@ extern "C" {
 int wfpt_wiener_like_multi(wfpt_ctx* c, const double* x, int64_t n,
                            const double* const arrays[7], const double scalars[7],
                            const wfpt_knobs* k, double p_outlier, double* out) {
+  return wfpt_wiener_like_multi_ex(c, x, n, arrays, scalars, k, p_outlier, out, nullptr);
+}
+
+int wfpt_wiener_like_multi_ex(wfpt_ctx* c, const double* x, int64_t n,
+                              const double* const arrays[7], const double scalars[7],
+                              const wfpt_knobs* k, double p_outlier, double* out,
+                              double* out_trial) {
   if (!c || (!x && n > 0) || !arrays || !scalars || !k || !out || n < 0)
     return fail(WFPT_ERR_ARG, "bad arguments");
   const wfpt::Knobs K = to_knobs(k);
+  WFPT_RANGE("wfpt_wiener_like_multi");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   if (int rc = upload(c, x, n)) return rc;
-  return run_multi(c, c->x.p, n, arrays, scalars, K, p_outlier, out);
+  return run_multi(c, c->x.p, n, arrays, scalars, K, p_outlier, out, out_trial);
 }
 
 int wfpt_wiener_like_multi_resident(wfpt_ctx* c, const wfpt_ds* d, const double* const arrays[7],
                                     const double scalars[7], const wfpt_knobs* k,
                                     double p_outlier, double* out) {
+  return wfpt_wiener_like_multi_resident_ex(c, d, arrays, scalars, k, p_outlier, out, nullptr);
+}
+
+int wfpt_wiener_like_multi_resident_ex(wfpt_ctx* c, const wfpt_ds* d,
+                                       const double* const arrays[7], const double scalars[7],
+                                       const wfpt_knobs* k, double p_outlier, double* out,
+                                       double* out_trial) {
   if (!c || !d || !arrays || !scalars || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
   if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
   if (!d->input_order || d->node)
@@ -887,9 +978,10 @@ int wfpt_wiener_like_multi_resident(wfpt_ctx* c, const wfpt_ds* d, const double*
                 "wiener_like_multi on a dataset needs one created with WFPT_DS_INPUT_ORDER "
                 "and no node ids (per-trial arrays follow the caller's trial order)");
   const wfpt::Knobs K = to_knobs(k);
+  WFPT_RANGE("wfpt_wiener_like_multi_resident");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  return run_multi(c, d->x, d->n, arrays, scalars, K, p_outlier, out);
+  return run_multi(c, d->x, d->n, arrays, scalars, K, p_outlier, out, out_trial);
 }
 
 int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
@@ -908,6 +1000,7 @@ int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_para
   const double epsi = 1e-10;
   const double par[7] = {a / 10., t, sv / 10. + epsi, z * (a / 10.), sz * (a / 10.) + epsi,
                          st + epsi, v / 10.};
+  WFPT_RANGE("wfpt_dmat_cdf_array");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   if (int rc = upload(c, x, n)) return rc;
@@ -957,51 +1050,204 @@ int wfpt_comm_init(wfpt_ctx* c, int nranks, int rank, const unsigned char id[128
   return WFPT_OK;
 }
 
+int wfpt_comm_init_tcp(wfpt_ctx* c, int nranks, int rank, const char* host, int port,
+                       int timeout_ms) {
+  if (!c || !host || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(WFPT_ERR_ARG, "bad communicator arguments");
+  WFPT_RANGE("wfpt_comm_init_tcp");
+  unsigned char id[128];
+  std::memset(id, 0, sizeof(id));
+  if (rank == 0)
+    if (int rc = wfpt_comm_unique_id(id)) return rc;
+  if (int rc = wfpt_comm_exchange_id(nranks, rank, host, port, timeout_ms, id)) return rc;
+  return wfpt_comm_init(c, nranks, rank, id);
+}
+
+int wfpt_comm_init_all(wfpt_ctx* const* ctxs, int n) {
+  if (!ctxs || n < 1) return fail(WFPT_ERR_ARG, "bad communicator arguments");
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i]) return fail(WFPT_ERR_ARG, "null context");
+    devs[i] = ctxs[i]->device;
+    for (int j = 0; j < i; ++j)
+      if (ctxs[j] == ctxs[i] || devs[j] == devs[i])
+        return fail(WFPT_ERR_ARG, "wfpt_comm_init_all: one context per distinct device");
+  }
+  WFPT_RANGE("wfpt_comm_init_all");
+  std::vector<ncclComm_t> comms(n, nullptr);
+  for (int i = 0; i < n; ++i) {
+    std::lock_guard<std::mutex> lk(ctxs[i]->mu);
+    if (ctxs[i]->comm) {
+      DeviceGuard g(ctxs[i]->device);
+      (void)ncclCommDestroy(ctxs[i]->comm);
+      ctxs[i]->comm = nullptr;
+    }
+  }
+  NCCL_TRY(ncclCommInitAll(comms.data(), n, devs.data()));
+  for (int i = 0; i < n; ++i) {
+    std::lock_guard<std::mutex> lk(ctxs[i]->mu);
+    ctxs[i]->comm = comms[i];
+    ctxs[i]->nranks = n;
+    ctxs[i]->rank = i;
+  }
+  return WFPT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+// One rank's local part of an all-reduce likelihood, in two steps so that a
+// single process can overlap its devices (wfpt_wiener_like_allreduce_group):
+// ar_launch enqueues the level-0 pass (+ the deferred pass unless the lean
+// prediction applies) whose finalize leaves {sum, #zeros, errors} in the
+// device buffer c->res.p; ar_settle waits for a lean call's level-0 result
+// and, on a misprediction, enqueues the redo + fold passes and a second
+// finalize over the intact chunk partials (an unconditional redo launch would
+// dispatch one wave per chunk: ~48k blocks at 12.5M trials). After ar_settle,
+// c->res.p holds the rank's triple in stream order.
+struct ArState {
+  bool eng = false, lean = false;
+};
+int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
+              ArState* st) {
+  HIP_TRY(c->res.reserve(6));
+  st->eng = engine_family(P, K);
+  st->lean = st->eng && c->lean && d->no_tree && !c->count;
+  if (st->lean)
+    return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d,
+                   c->res.p);
+  return run_sum(c, d->x, d->n, P, K, c->res.p, wfpt::kPassAll, d);
+}
+int ar_settle(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
+              const ArState& st) {
+  if (!st.lean) return WFPT_OK;
+  if (int rc = wait_result(c, c->mres)) return rc;
+  if (res_deferred(c->mres))
+    return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassDeferred | wfpt::kPassRedo, d,
+                   c->res.p);
+  return WFPT_OK;
+}
+// After the exchange: the summed triple to the mapped slot with a fresh
+// completion word (the local finalize used the previous one), then decode.
+int ar_finish(wfpt_ctx* c, const wfpt_ds* d, const ArState& st, double* out) {
+  wfpt::launch_publish(c->res.p, c->mres_dev, ++c->seq, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (int rc = wait_result(c, c->mres)) return rc;
+  split_advance(d, st.eng && !st.lean, c->mres);
+  const int rc = decode_sum(c, c->mres, out);
+  if (rc == WFPT_OK && st.eng) d->no_tree = !res_tree(c->mres);
+  return rc;
+}
+}  // namespace
+
+extern "C" {
+
 int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
                                const wfpt_knobs* k, double* out) {
   if (!c || !d || !p || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
   if (!c->comm) return fail(WFPT_ERR_ARG, "wfpt_comm_init was not called");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
   const wfpt::Params P = to_params(p);
   const wfpt::Knobs K = to_knobs(k);
   if (!p_outlier_in_range(P.p_outlier)) {  // uniform on every rank: no exchange needed
     *out = -INFINITY;
     return WFPT_OK;
   }
+  WFPT_RANGE("wfpt_wiener_like_allreduce");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
-  HIP_TRY(c->res.reserve(6));
-  const bool eng = engine_family(P, K);
-  const bool lean = eng && c->lean && d->no_tree && !c->count;
-  if (lean) {
-    // the lean prediction settles the local sum before the exchange: level-0
-    // pass + finalize (result to the mapped slot and to the device buffer the
-    // exchange reads); a misprediction adds the redo + fold passes and a second
-    // finalize after one host round trip (an unconditional redo launch would
-    // dispatch one wave per chunk: ~48k blocks at 12.5M trials)
-    if (int rc = run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d,
-                         c->res.p))
-      return rc;
-    if (int rc = wait_result(c, c->mres)) return rc;
-    if (res_deferred(c->mres)) {
-      if (int rc = run_sum(c, d->x, d->n, P, K, c->mres_dev,
-                           wfpt::kPassDeferred | wfpt::kPassRedo, d, c->res.p))
-        return rc;
+  ArState st;
+  int lrc = ar_launch(c, d, P, K, &st);
+  if (lrc == WFPT_OK) lrc = ar_settle(c, d, P, K, st);
+  // fault injection for the failure path's tests (WFPT_FAULT=allreduce_local:
+  // this rank's local pass reports a failure after it ran)
+  if (lrc == WFPT_OK) {
+    const char* fi = std::getenv("WFPT_FAULT");
+    if (fi && std::strcmp(fi, "allreduce_local") == 0)
+      lrc = fail(WFPT_ERR_HIP, "injected local failure (WFPT_FAULT=allreduce_local)");
+  }
+  std::string lmsg;
+  if (lrc != WFPT_OK) {
+    // A rank that failed locally still enters the collective, with a
+    // poisoned triple (kPeerFailUnit), so that no peer waits on it forever;
+    // every peer then decodes "a rank failed" and this rank returns its own
+    // error. Only a broken stream (a sticky device fault) cannot enqueue the
+    // exchange: the communicator is then aborted.
+    lmsg = g_last_error;
+    double poison[3];
+    wfpt_result_poison(poison);
+    const hipError_t e = c->res.p ? hipMemcpyAsync(c->res.p, poison, sizeof(poison),
+                                                    hipMemcpyHostToDevice, c->stream)
+                                  : hipErrorInvalidValue;
+    if (e != hipSuccess) {
+      (void)ncclCommAbort(c->comm);
+      c->comm = nullptr;
+      return fail(lrc, lmsg + " (device stream unusable: RCCL communicator aborted; "
+                              "re-create it with wfpt_comm_init)");
     }
-  } else if (int rc = run_sum(c, d->x, d->n, P, K, c->res.p, wfpt::kPassAll, d)) {
-    return rc;
   }
   // {sum, zeros, encoded errors} of every rank summed: any zero trial or
-  // failure anywhere reaches every rank (the error encoding keeps depth and
-  // budget failures apart under the sum, wfpt_internal.h: kBudgetUnit)
+  // failure anywhere reaches every rank (wfpt_internal.h: the error counts
+  // stay apart under the sum)
   NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 3, ncclDouble, ncclSum, c->comm, c->stream));
-  // the summed result goes to the mapped slot with a fresh completion word
-  // (run_sum's finalize used the previous one for the device copy)
-  wfpt::launch_publish(c->res.p, c->mres_dev, ++c->seq, c->stream);
-  HIP_TRY(hipGetLastError());
-  if (int rc = wait_result(c, c->mres)) return rc;
-  split_advance(d, eng && !lean, c->mres);
-  const int rc = decode_sum(c, c->mres, out);
-  if (rc == WFPT_OK && eng) d->no_tree = !res_tree(c->mres);
+  if (lrc != WFPT_OK) {
+    (void)hipStreamSynchronize(c->stream);
+    return fail(lrc, lmsg);
+  }
+  return ar_finish(c, d, st, out);
+}
+
+int wfpt_wiener_like_allreduce_group(wfpt_ctx* const* ctxs, const wfpt_ds* const* dss, int n,
+                                     const wfpt_params* p, const wfpt_knobs* k, double* out) {
+  if (!ctxs || !dss || n < 1 || !p || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i] || !dss[i]) return fail(WFPT_ERR_ARG, "null context or dataset");
+    if (dss[i]->ctx != ctxs[i]) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+    if (!ctxs[i]->comm || ctxs[i]->nranks != n || ctxs[i]->rank != i)
+      return fail(WFPT_ERR_ARG, "contexts need wfpt_comm_init_all over the same list");
+  }
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (!p_outlier_in_range(P.p_outlier)) {
+    *out = -INFINITY;
+    return WFPT_OK;
+  }
+  WFPT_RANGE("wfpt_wiener_like_allreduce_group");
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (int i = 0; i < n; ++i) locks.emplace_back(ctxs[i]->mu);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  std::vector<ArState> st(n);
+  // every device's local pass in flight before any wait; a failure on any
+  // device ends the call before the collective (no device has entered it)
+  int rc = WFPT_OK;
+  for (int i = 0; i < n && rc == WFPT_OK; ++i) {
+    (void)hipSetDevice(ctxs[i]->device);
+    rc = ar_launch(ctxs[i], dss[i], P, K, &st[i]);
+  }
+  for (int i = 0; i < n && rc == WFPT_OK; ++i) {
+    (void)hipSetDevice(ctxs[i]->device);
+    rc = ar_settle(ctxs[i], dss[i], P, K, st[i]);
+  }
+  if (rc == WFPT_OK) {
+    ncclResult_t r = ncclGroupStart();
+    for (int i = 0; i < n && r == ncclSuccess; ++i)
+      r = ncclAllReduce(ctxs[i]->res.p, ctxs[i]->res.p, 3, ncclDouble, ncclSum, ctxs[i]->comm,
+                        ctxs[i]->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess)
+      rc = fail(WFPT_ERR_COMM, std::string("ncclAllReduce (group): ") + ncclGetErrorString(r));
+  }
+  double v = 0.0;
+  for (int i = 0; i < n && rc == WFPT_OK; ++i) {
+    (void)hipSetDevice(ctxs[i]->device);
+    double vi = 0.0;
+    rc = ar_finish(ctxs[i], dss[i], st[i], &vi);
+    if (i == 0) v = vi;
+  }
+  (void)hipSetDevice(prev);
+  if (rc == WFPT_OK) *out = v;
   return rc;
 }
 

@@ -687,6 +687,23 @@ __device__ inline Trial trial_setup(double x, const Params& P) {
   return T;
 }
 
+// trial_setup for a trial whose boundary is known to the caller (flip ==
+// (x > 0)): the same values, but v and z come from `flip` alone, so inside a
+// pass over one boundary (flip wave-uniform) they are wave-uniform too.
+__device__ inline Trial trial_setup_b(double x, const Params& P, bool flip) {
+  Trial T;
+  const double a = P.a, sv = P.sv, t = P.t, st0 = P.st, sz0 = P.sz;
+  T.valid = !((P.z < 0) || (P.z > 1) || (a < 0) || (t < 0) || (st0 < 0) || (sv < 0) ||
+              (sz0 < 0) || (sz0 > 1) || ((fabs(x) - (t - st0 / 2.)) < 0) ||
+              (P.z + sz0 / 2. > 1) || (P.z - sz0 / 2. < 0) || (t - st0 / 2. < 0));
+  T.v = flip ? -P.v : P.v;
+  T.z = flip ? 1. - P.z : P.z;
+  T.x = fabs(x);
+  T.st = (st0 < 1e-3) ? 0.0 : st0;
+  T.sz = (sz0 < 1e-3) ? 0.0 : sz0;
+  return T;
+}
+
 // full_pdf (pdf.pxi:104-146) for one trial: the general per-lane walk (the
 // fallback for trees deeper than the breadth-first levels, fixed Simpson,
 // per-trial parameters). MODE is the integration family (kRuntime: per lane).
@@ -884,6 +901,23 @@ __device__ inline double exp_val(double x) {
 #endif
 }
 
+// Element i (a run-time index) of a 5-element register array, and its store:
+// selects, so the array stays in registers inside a non-unrolled loop.
+// Written out with constant subscripts (no loop): every access is a constant
+// index from the start, so the array is split into registers, never
+// promoted to memory.
+__device__ inline double pick5(const double (&v)[5], int i) {
+  const double a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3], a4 = v[4];
+  return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : i == 3 ? a3 : a4;
+}
+__device__ inline void put5(double (&v)[5], int i, double x) {
+  v[0] = i == 0 ? x : v[0];
+  v[1] = i == 1 ? x : v[1];
+  v[2] = i == 2 ? x : v[2];
+  v[3] = i == 3 ? x : v[3];
+  v[4] = i == 4 ? x : v[4];
+}
+
 // pdf_sv at the 5 root-level z nodes of one t node (the values of
 // tnode_pdf_sv at each node to a few ulp):
 //   * small-t series: the exponents (g_j + 2k)^2 m are quadratic in j on the
@@ -893,7 +927,7 @@ __device__ inline double exp_val(double x) {
 //   * large-t series: the Chebyshev recurrence in k from the rotated sin/cos;
 //   * the drift factor exp(c_j): three exponentials and the second-difference
 //     recurrence (direct exps when |c| > 600).
-__device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
+__device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
                                           double a, double (&out)[5]) {
   double p[5];
 #pragma unroll
@@ -901,7 +935,7 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
   if (!T.pos) {
 #pragma unroll
     for (int i = 0; i < 5; ++i) out[i] = 0.0;
-    return;
+    return true;
   }
   const int K = T.K;
   if (T.small) {
@@ -911,29 +945,36 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     bool have_q = false;
     for (int k = lower; k <= upper; ++k) {
       const double k2 = (double)(2 * k);
-      double wk[5], ek[5];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        wk[i] = G.g[i] + k2;
-        ek[i] = (wk[i] * wk[i]) * T.m;
-      }
-      if (ek[0] > -600.0 && ek[4] > -600.0) {  // ek <= 0 and convex in j: ends are the minima
-        const double d1 = ek[1] - ek[0];
+      // ek_j = (g_j + 2k)^2 m <= 0 is convex in j: the ends are the minima.
+      // Operands are formed where they are used (the grid is wave-uniform in
+      // the lean pass), not held as arrays across the branch.
+      const double w0 = G.g[0] + k2, w4 = G.g[4] + k2;
+      const double e0 = (w0 * w0) * T.m, e4 = (w4 * w4) * T.m;
+      if (e0 > -600.0 && e4 > -600.0) {
+        const double w1 = G.g[1] + k2, w2 = G.g[2] + k2;
+        const double e1 = (w1 * w1) * T.m, e2 = (w2 * w2) * T.m;
+        const double d1 = e1 - e0;
         if (!have_q) {
-          qq = exp_val((ek[2] - ek[1]) - d1);
+          qq = exp_val((e2 - e1) - d1);
           have_q = true;
         }
-        double E = exp_val(ek[0]);
+        double E = exp_val(e0);
         double R = exp_val(d1);
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-          p[i] = madd(wk[i], E, p[i]);
+          p[i] = madd(G.g[i] + k2, E, p[i]);
           E = E * R;
           R = R * qq;
         }
       } else {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) p[i] = madd(wk[i], exp_val(ek[i]), p[i]);
+        // rare (an end exponent in subnormal territory): one node per trip,
+        // so the hot path's register allocation does not carry five
+        // interleaved exponentials
+#pragma unroll 1
+        for (int i = 0; i < 5; ++i) {
+          const double wi = pick5(G.g, i) + k2;
+          put5(p, i, madd(wi, exp_val((wi * wi) * T.m), pick5(p, i)));
+        }
       }
     }
 #pragma unroll
@@ -984,18 +1025,20 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = p[i] * kPi;
   }
-  // exponent of the drift factor at each node (quadratic in g)
-  double cexp[5];
-#pragma unroll
-  for (int i = 0; i < 5; ++i)
-    cexp[i] = (sv == 0) ? G.A[i] - (T.vvx * 0.5) : (G.A[i] - T.vvx) * T.cden;
+  // exponent of the drift factor at each node (quadratic in g), formed where
+  // it is used
+  auto cexp = [&](int i) -> double {
+    return (sv == 0) ? G.A[i] - (T.vvx * 0.5) : (G.A[i] - T.vvx) * T.cden;
+  };
   double ex[5];
-  const bool moderate = fabs(cexp[0]) < 600.0 && fabs(cexp[2]) < 600.0 && fabs(cexp[4]) < 600.0;
+  const double c0 = cexp(0), c2 = cexp(2), c4 = cexp(4);
+  const bool moderate = fabs(c0) < 600.0 && fabs(c2) < 600.0 && fabs(c4) < 600.0;
   if (moderate) {
     // c_j = c0 + j d1 + j(j-1)/2 d2  ->  E_j = E_{j-1} * R * Q^(j-1)
-    const double d1 = cexp[1] - cexp[0];
-    const double d2 = (cexp[2] - cexp[1]) - d1;
-    ex[0] = exp_val(cexp[0]);
+    const double c1 = cexp(1);
+    const double d1 = c1 - c0;
+    const double d2 = (c2 - c1) - d1;
+    ex[0] = exp_val(c0);
     double rr = exp_val(d1);
     const double qd = exp_val(d2);
 #pragma unroll
@@ -1003,9 +1046,12 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
       ex[j] = ex[j - 1] * rr;
       rr = rr * qd;
     }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) ex[i] = exp_val(cexp[i]);
+  } else {  // rare: one node per trip (register allocation as above)
+#pragma unroll 1
+    for (int i = 0; i < 5; ++i) {
+      const double Ai = pick5(G.A, i);
+      put5(ex, i, exp_val((sv == 0) ? Ai - (T.vvx * 0.5) : (Ai - T.vvx) * T.cden));
+    }
   }
   // the common case: every series value positive and every product finite;
   // the rare fix-ups below run only on lanes that need one (same values)
@@ -1015,7 +1061,8 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     out[i] = (p[i] * ex[i]) * T.sc;
     clean = clean & (p[i] > 0) & !__builtin_isinf(out[i]);
   }
-  if (__builtin_expect(clean, 1)) return;
+  if (__builtin_expect(clean, 1)) return true;
+  bool ok = true;
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     double r2 = out[i];
@@ -1023,12 +1070,12 @@ __device__ inline void tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     // exp(log 0 + c) = 0 even if e^c = inf; 0 * sc keeps the reference's
     // 0 / (a*a) = NaN at a == 0
     if (p[i] == 0) r2 = 0.0 * T.sc;
+    // exp(c) overflow with a finite true value: the reference's literal
+    // exp(log p + c) is the exact path's (the caller routes the trial there)
+    ok = ok & !(__builtin_isinf(r2) && p[i] > 0);
     out[i] = r2;
   }
-  // exp(c) overflow: the reference's literal exp(log p + c) (rare, per lane)
-#pragma unroll
-  for (int i = 0; i < 5; ++i)
-    if (__builtin_isinf(out[i]) && p[i] > 0) out[i] = tnode_pdf_sv(T, G.g[i], v, sv, a);
+  return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -1088,7 +1135,7 @@ __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, 
                                     double sv, double a, const Knobs& K, int& flags,
                                     long long& ne, bool& repair) {
   double f[5];
-  tnode_pdf_sv_grid5(T, G, v, sv, a, f);
+  if (!tnode_pdf_sv_grid5(T, G, v, sv, a, f)) flags |= kFlagExact;
 #pragma unroll
   for (int i = 0; i < 5; ++i) f[i] = f[i] * iZz;
   ne += 5;
@@ -1222,9 +1269,9 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
 // The engine's level 0 of one trial (as fast_level0, on the table's z grid):
 // kFinal (p), kTree (f[], pend) or kExact.
 template <int MODE>
-__device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
-                                 double& p, double (&f)[5], long long& ne, unsigned& pend) {
-  const Trial tr = trial_setup(x0, P);
+__device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs& K,
+                                   const ZGrid& G, double& p, double (&f)[5], long long& ne,
+                                   unsigned& pend) {
   p = 0.0;
   pend = 0u;
   if (!tr.valid) return kFinal;
@@ -1235,7 +1282,7 @@ __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, con
     const double iw = 1.0 / (ub - lb);
     const TNode T = tnode_setup(tr.x - P.t, tr.v, P.sv, P.a, K.err);
     if (T.amb) return kExact;
-    tnode_pdf_sv_grid5(T, G, tr.v, P.sv, P.a, f);
+    if (!tnode_pdf_sv_grid5(T, G, tr.v, P.sv, P.a, f)) return kExact;
 #pragma unroll
     for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
     ne += 5;
@@ -1263,6 +1310,11 @@ __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, con
   p = s.S2 + (s.S2 - s.S) / 15;
   const bool structural = (MODE == kAdaptZ) ? tr.x - P.t <= 0 : tr.x - lb <= 0;
   return (p > kExactBelow || structural) ? kFinal : kExact;
+}
+template <int MODE>
+__device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
+                                 double& p, double (&f)[5], long long& ne, unsigned& pend) {
+  return eng_level0_t<MODE>(trial_setup(x0, P), P, K, G, p, f, ne, pend);
 }
 
 // z grids of the engine, relative to the dyadic points P of [lb_z, ub_z]:

@@ -12,8 +12,9 @@
 //   * an adaptive stop test |S2 - S| <= 15 err sits inside kTieBand of its
 //     threshold (the fast path's values carry ~1e-14 relative error);
 //   * fixed Simpson (use_adaptive = 0) gives such a density.
-// Host and device (WFPT_HD): tests/test_exact_path.py compiles it with gcc and
-// compares it with the oracle bit for bit.
+// Host and device (WFPT_HD): tests/test_exact_path.py compiles it with gcc
+// (tests/c/exact_host.cpp) and compares it with the reference fixtures and the
+// oracle (bit for bit except where glibc misrounds).
 #pragma once
 #include "wfpt_crlibm.hpp"
 

@@ -56,8 +56,12 @@ struct Split {
 };
 
 // Error flags encoded as counts in one double that survives an RCCL sum:
-// (#ranks with a depth error) + kBudgetUnit * (#ranks with a budget error).
+// (#ranks with a depth error) + kBudgetUnit * (#ranks with a budget error)
+// + kPeerFailUnit * (#ranks whose local pass failed before the exchange: a
+// failing rank still enters the collective with this poisoned count, so no
+// peer waits on it forever). All sums stay exact integers in a double.
 constexpr double kBudgetUnit = 1048576.0;
+constexpr double kPeerFailUnit = 1099511627776.0;  // 2^40
 
 int stack_kind(const Knobs& K);
 int64_t blocks_for(int64_t n);
@@ -114,9 +118,10 @@ void launch_multi_fast(int mode, const double* x, int64_t n, const double* const
                        const double* scal, const Knobs& K, double p_outlier, double* lp,
                        int64_t* d_idx, Params* d_par, int* n_defer, double* part, int* zeros,
                        unsigned long long* evals, int* status, hipStream_t s);
+// lp (nullable): each trial's term too
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
                   const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
-                  hipStream_t s);
+                  hipStream_t s, double* lp = nullptr);
 // cdfdif_kernels.hip: dmat_cdf_array over device x[n]; par = the wrapper's
 // transformed (a, Ter, eta, z, sZ, st, nu) (cdfdif_wrapper.pyx:36-42).
 // defer: n ints of workspace, n_defer: one device int.

@@ -42,7 +42,7 @@ static inline int64_t fast_blocks(int64_t n) { return (n + kFastBlock - 1) / kFa
 #define WFPT_FAST_WAVES 3
 #endif
 #ifndef WFPT_FAST_WAVES_TZ
-#define WFPT_FAST_WAVES_TZ 2
+#define WFPT_FAST_WAVES_TZ 3
 #endif
 template <int MODE>
 struct FastWaves {
@@ -431,7 +431,8 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
       const TNode T = tnode_setup_r(xx, vo, sv, a, ia2, err, qh, known, kd);
       if (T.amb) atomicOr(&cl.fl[owner], (int)kFlagExact);
       if (MODE == kAdaptT) y[0] = tnode_pdf_sv(T, flip ? 1. - z : z, vo, sv, a);
-      else tnode_pdf_sv_grid5(T, cl.tab.G[flip][gs], vo, sv, a, y);
+      else if (!tnode_pdf_sv_grid5(T, cl.tab.G[flip][gs], vo, sv, a, y))
+        atomicOr(&cl.fl[owner], (int)kFlagExact);  // exp(c) overflow: the exact path
     }
     if (stage == 0) {
       bool pend = false;
@@ -745,23 +746,26 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
 // engine would (chunk_out). A chunk with a refining trial writes nothing but
 // its redo flag and a nonzero deferred count; the engine's redo pass
 // (kPassRedo) then processes it from scratch, as a full engine call would.
-__device__ inline ZGrid zgrid_pick(const RootGrids& R, bool pos) {
+// Root z grid of boundary b (0: lower, 1: upper) with b wave-uniform: every
+// field is a select between two kernel arguments on a uniform condition, so
+// the grid stays in scalar registers.
+__device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
   const ZGrid& g0 = R.G[0];
   const ZGrid& g1 = R.G[1];
   ZGrid G;
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
-    G.g[k] = pos ? g1.g[k] : g0.g[k];
-    G.A[k] = pos ? g1.A[k] : g0.A[k];
+    G.g[k] = b ? g1.g[k] : g0.g[k];
+    G.A[k] = b ? g1.A[k] : g0.A[k];
   }
-  G.h6 = pos ? g1.h6 : g0.h6;
-  G.h12 = pos ? g1.h12 : g0.h12;
-  G.s0 = pos ? g1.s0 : g0.s0;
-  G.c0 = pos ? g1.c0 : g0.c0;
-  G.s4 = pos ? g1.s4 : g0.s4;
-  G.c4 = pos ? g1.c4 : g0.c4;
-  G.sd = pos ? g1.sd : g0.sd;
-  G.cd = pos ? g1.cd : g0.cd;
+  G.h6 = b ? g1.h6 : g0.h6;
+  G.h12 = b ? g1.h12 : g0.h12;
+  G.s0 = b ? g1.s0 : g0.s0;
+  G.c0 = b ? g1.c0 : g0.c0;
+  G.s4 = b ? g1.s4 : g0.s4;
+  G.c4 = b ? g1.c4 : g0.c4;
+  G.sd = b ? g1.sd : g0.sd;
+  G.cd = b ? g1.cd : g0.cd;
   return G;
 }
 
@@ -778,7 +782,22 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   long long ne0 = 0;
   unsigned pend0 = 0u;
   int oc = kFinal;
-  if (own) oc = eng_level0<MODE>(x0, A.P, A.K, zgrid_pick(R, x0 > 0), p, f0, ne0, pend0);
+  // The wave's trials by boundary. Inside one boundary the root z grid and
+  // the flipped v, z (pdf.pxi:116-118) are wave-uniform: they stay in scalar
+  // registers (zgrid_uniform) instead of per-lane selects and copies.
+  // Datasets are ordered by boundary, then |rt| (wfpt_dataset_create), so
+  // only the wave at the boundary switch is mixed: its upper-boundary lanes
+  // take the second call site.
+  const bool pos = x0 > 0;
+  const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
+  const int b = (bp == bo) ? 1 : 0;  // every trial upper: 1; otherwise lower first
+  if (own && pos == (b != 0))
+    oc = eng_level0_t<MODE>(trial_setup_b(x0, A.P, b != 0), A.P, A.K, zgrid_uniform(R, b), p,
+                            f0, ne0, pend0);
+  if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
+    if (own && pos)
+      oc = eng_level0_t<MODE>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0, ne0, pend0);
+  }
   if (__ballot(oc == kTree) != 0ull) {
     if (lane == 0) {
       W.redo[c] = 1;
@@ -1258,7 +1277,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(
 template <int STK>
 __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(
     const double* x, int64_t n, const double* const* arr, const double* scal, Knobs K,
-    double p_outlier, double* out, int* zeros, int* status) {
+    double p_outlier, double* out, int* zeros, int* status, double* lpo) {
   using Stack = typename StackOf<STK>::type;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double lp = 0.0;
@@ -1291,6 +1310,7 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(
     }
     // the reference has no early exit here: log(0) = -inf enters the sum
     lp = log(p);
+    if (lpo) lpo[i] = lp;
   }
   block_reduce<false>(lp, zero, ne);
   if (threadIdx.x == 0) {
@@ -1632,19 +1652,19 @@ void launch_multi_fast(int mode, const double* x, int64_t n, const double* const
 
 void launch_multi(const double* x, int64_t n, const double* const* arr, const double* scal,
                   const Knobs& K, double p_outlier, double* part, int* zeros, int* status,
-                  hipStream_t s) {
+                  hipStream_t s, double* lp) {
   const int64_t nb = blocks_for(n);
   if (nb == 0) return;
   const int stk = stack_kind(K);
   if (stk == 0)
     hipLaunchKernelGGL((multi_kernel<0>), dim3(nb), dim3(kBlock), 0, s, x, n, arr, scal, K,
-                       p_outlier, part, zeros, status);
+                       p_outlier, part, zeros, status, lp);
   else if (stk == 1)
     hipLaunchKernelGGL((multi_kernel<1>), dim3(nb), dim3(kBlock), 0, s, x, n, arr, scal, K,
-                       p_outlier, part, zeros, status);
+                       p_outlier, part, zeros, status, lp);
   else
     hipLaunchKernelGGL((multi_kernel<2>), dim3(nb), dim3(kBlock), 0, s, x, n, arr, scal, K,
-                       p_outlier, part, zeros, status);
+                       p_outlier, part, zeros, status, lp);
 }
 
 }  // namespace wfpt

@@ -121,6 +121,24 @@ def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=
     return out.value
 
 
+def wiener_like_multi_terms(x, v, sv, a, z, sz, t, st, err, multi, n_st=10, n_sz=10,
+                            use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0):
+    """wiener_like_multi (wfpt.pyx:244-274) returning (sum, per-trial terms):
+    terms[i] is trial i's addend log p_i (wfpt.pyx:261-272)."""
+    x = _check_x(x)
+    n = x.shape[0]
+    ptrs, scal, keep = _multi_args(n, v, sv, a, z, sz, t, st, multi)
+    c = _lib.context()
+    K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+    out = ctypes.c_double()
+    terms = np.empty(n, dtype=np.float64)
+    _lib.check(_lib.wfpt_wiener_like_multi_ex(c.handle, _lib.dptr(x), n, ptrs, _lib.dptr(scal),
+                                              ctypes.byref(K), float(p_outlier),
+                                              ctypes.byref(out), _lib.dptr(terms)))
+    del keep
+    return out.value, terms
+
+
 def gen_rts_from_cdf(v, sv, a, z, sz, t, st, samples=1000, cdf_lb=-6, cdf_ub=6, dt=1e-2):
     """wfpt.pyx:323-354: inverse-CDF sampling from the density on a dt grid.
 
@@ -207,7 +225,7 @@ class Dataset:
 
     def wiener_like_allreduce(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10,
                               use_adaptive=1, simps_err=1e-8, p_outlier=0, w_outlier=0.1):
-        """Global sum over every rank's shard (requires hddm_amd.dist.init_comm)."""
+        """Global sum over every rank's shard (requires hddm_amd.dist.init_comm; torch-free)."""
         P = _lib.make_params(v, sv, a, z, sz, t, st, p_outlier)
         K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = ctypes.c_double()
@@ -217,23 +235,27 @@ class Dataset:
         return out.value
 
     def wiener_like_multi(self, v, sv, a, z, sz, t, st, err, multi, n_st=10, n_sz=10,
-                          use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0):
+                          use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0,
+                          trials=False):
         """wiener_like_multi (wfpt.pyx:244-274) over this resident dataset
         (created with input_order=True): only the per-trial parameter arrays
-        go to the device per call."""
+        go to the device per call. trials=True: (sum, per-trial terms)."""
         ptrs, scal, keep = _multi_args(self.n, v, sv, a, z, sz, t, st, multi)
         K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = ctypes.c_double()
-        _lib.check(_lib.wfpt_wiener_like_multi_resident(
+        terms = np.empty(self.n, dtype=np.float64) if trials else None
+        _lib.check(_lib.wfpt_wiener_like_multi_resident_ex(
             self.ctx.handle, self.handle, ptrs, _lib.dptr(scal), ctypes.byref(K),
-            float(p_outlier), ctypes.byref(out)))
+            float(p_outlier), ctypes.byref(out), _lib.dptr(terms) if trials else None))
         del keep
-        return out.value
+        return (out.value, terms) if trials else out.value
 
     def wiener_like_nodes(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
-                          simps_err=1e-3, w_outlier=0.1):
+                          simps_err=1e-3, w_outlier=0.1, trials=False):
         """params: array (n_nodes, 8) of v, sv, a, z, sz, t, st, p_outlier.
-        Returns the per-node summed log-likelihoods (float64[n_nodes])."""
+        Returns the per-node summed log-likelihoods (float64[n_nodes]);
+        trials=True: (per-node sums, per-trial log terms in the order the
+        trials were given to the Dataset)."""
         if self.n_nodes == 0:
             raise ValueError("dataset was created without node ids")
         pm = np.ascontiguousarray(np.asarray(params, dtype=np.float64))
@@ -242,6 +264,12 @@ class Dataset:
         table = (_lib.Params * self.n_nodes).from_buffer_copy(pm.tobytes())
         K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = np.empty(self.n_nodes, dtype=np.float64)
+        if trials:
+            terms = np.empty(self.n, dtype=np.float64)
+            _lib.check(_lib.wfpt_wiener_like_nodes_ex(self.ctx.handle, self.handle, table,
+                                                      ctypes.byref(K), _lib.dptr(out),
+                                                      _lib.dptr(terms)))
+            return out, terms
         _lib.check(_lib.wfpt_wiener_like_nodes(self.ctx.handle, self.handle, table,
                                                ctypes.byref(K), _lib.dptr(out)))
         return out

@@ -103,6 +103,13 @@ int wfpt_wiener_like_host(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_
  * out_logp[n_nodes] out (each = wiener_like of that node's trials). */
 int wfpt_wiener_like_nodes(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *per_node,
                            const wfpt_knobs *k, double *out_logp);
+/* As wfpt_wiener_like_nodes; out_trial (nullable, ds size) also receives
+ * each trial's log term, in the order the caller passed the trials to
+ * wfpt_dataset_create: log of the node's mixture p (1 - p_outlier) +
+ * w_outlier p_outlier, -inf for a zero mixture density or a p_outlier outside
+ * [0, 1] (wfpt.pyx:63-72 per node). */
+int wfpt_wiener_like_nodes_ex(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *per_node,
+                              const wfpt_knobs *k, double *out_logp, double *out_trial);
 /* Per-trial mixture density, or its log if logp != 0 (wfpt.pyx:32-48). */
 int wfpt_pdf_array(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
                    const wfpt_knobs *k, int logp, double *out);
@@ -115,12 +122,22 @@ int wfpt_full_pdf(wfpt_ctx *ctx, double x, const wfpt_params *p, const wfpt_knob
 int wfpt_wiener_like_multi(wfpt_ctx *ctx, const double *x, int64_t n,
                            const double *const arrays[7], const double scalars[7],
                            const wfpt_knobs *k, double p_outlier, double *out_logp);
+/* As wfpt_wiener_like_multi; out_trial (nullable, n values) also receives
+ * each trial's term of the sum (wfpt.pyx:261-272), in trial order. */
+int wfpt_wiener_like_multi_ex(wfpt_ctx *ctx, const double *x, int64_t n,
+                              const double *const arrays[7], const double scalars[7],
+                              const wfpt_knobs *k, double p_outlier, double *out_logp,
+                              double *out_trial);
 /* Same over a resident dataset created with WFPT_DS_INPUT_ORDER (the RTs of a
  * regression model stay fixed across MCMC; only the per-trial parameter
  * arrays, hddm_regression.py:26-36, go up per call). */
 int wfpt_wiener_like_multi_resident(wfpt_ctx *ctx, const wfpt_ds *ds,
                                     const double *const arrays[7], const double scalars[7],
                                     const wfpt_knobs *k, double p_outlier, double *out_logp);
+int wfpt_wiener_like_multi_resident_ex(wfpt_ctx *ctx, const wfpt_ds *ds,
+                                       const double *const arrays[7], const double scalars[7],
+                                       const wfpt_knobs *k, double p_outlier, double *out_logp,
+                                       double *out_trial);
 
 /* ---- DMAT / Tuerlinckx CDF ---------------------------------------------- */
 /* Per-trial CDF of signed RTs with the outlier mixture, exactly
@@ -131,25 +148,53 @@ int wfpt_wiener_like_multi_resident(wfpt_ctx *ctx, const wfpt_ds *ds,
 int wfpt_dmat_cdf_array(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
                         double w_outlier, double *out);
 
-/* ---- multi-GPU (one process per GPU, RCCL over xGMI) -------------------- */
-/* 128-byte RCCL unique id, created on rank 0 and broadcast by the caller. */
+/* ---- multi-GPU: trials sharded over GPUs, RCCL all-reduce over xGMI ----- */
+/* (The reference has no multi-device path; SURVEY.md §8(e). Every entry point
+ * below is new, combining per-shard wiener_like sums, src/wfpt.pyx:66-76.) */
+/* One process per GPU. The 128-byte RCCL unique id is created on rank 0 and
+ * handed to every rank, either by the caller (wfpt_comm_init) or by the
+ * library's own TCP rendezvous: rank 0 listens on host:port and sends the id
+ * to each rank that connects (wfpt_comm_exchange_id; no GPU, no PyTorch). */
 int wfpt_comm_unique_id(unsigned char id[128]);
 int wfpt_comm_init(wfpt_ctx *ctx, int nranks, int rank, const unsigned char id[128]);
+int wfpt_comm_exchange_id(int nranks, int rank, const char *host, int port, int timeout_ms,
+                          unsigned char id[128]);
+/* unique id on rank 0 + wfpt_comm_exchange_id + wfpt_comm_init */
+int wfpt_comm_init_tcp(wfpt_ctx *ctx, int nranks, int rank, const char *host, int port,
+                       int timeout_ms);
 /* wiener_like over this rank's resident shard, combined across ranks with one
  * ncclAllReduce of 3 doubles {sum log p, #zero-density trials, encoded error
  * counts}; every rank receives the global total (-inf if any rank holds a
- * zero-density trial) or every rank fails with the same WFPT_ERR_UNSUPPORTED
- * if any rank exceeded the depth / evaluation limits. */
+ * zero-density trial) or every rank fails: WFPT_ERR_UNSUPPORTED if some rank
+ * exceeded the depth / evaluation limits; a rank whose local pass failed
+ * returns its own error after entering the exchange with a poisoned triple
+ * (wfpt_result_poison), and its peers return WFPT_ERR_COMM — no rank is left
+ * waiting in the collective. A broken device stream (sticky fault) cannot
+ * enter it: that rank aborts its communicator. */
 int wfpt_wiener_like_allreduce(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
                                const wfpt_knobs *k, double *out_logp);
+/* One process driving n GPUs (e.g. a single PyMC sampler): ctxs[i] (distinct
+ * devices) get one communicator each from ncclCommInitAll; dss[i] is the i-th
+ * shard, resident on ctxs[i]. The group call overlaps the devices' level-0
+ * passes and issues the n all-reduces inside one ncclGroupStart/End; a local
+ * failure on any device ends the call before the collective. */
+int wfpt_comm_init_all(wfpt_ctx *const *ctxs, int n);
+int wfpt_wiener_like_allreduce_group(wfpt_ctx *const *ctxs, const wfpt_ds *const *dss, int n,
+                                     const wfpt_params *p, const wfpt_knobs *k,
+                                     double *out_logp);
+/* The triple a rank that failed before the exchange contributes: {0, 0,
+ * 2^40} (one "failed rank" unit; see wfpt_decode_result). */
+int wfpt_result_poison(double r[3]);
 
 /* Decodes a likelihood result triple {sum of log p over trials with nonzero
  * density, #zero-density trials, encoded error counts} — the 3 doubles that
  * wfpt_wiener_like_allreduce sums over ranks — into the reference's value:
  * -inf if any trial had zero density (wfpt.pyx:71-72), else the sum; a nonzero
- * error count returns WFPT_ERR_UNSUPPORTED naming each error kind. Error
- * encoding: (#ranks past WFPT_MAX_DEPTH) + 1048576 * (#ranks past
- * WFPT_EVAL_BUDGET), so kinds stay apart under the sum. */
+ * error count returns an error naming each kind: WFPT_ERR_UNSUPPORTED for the
+ * depth / budget limits, WFPT_ERR_COMM when only failed ranks are counted.
+ * Error encoding: (#ranks past WFPT_MAX_DEPTH) + 2^20 * (#ranks past
+ * WFPT_EVAL_BUDGET) + 2^40 * (#ranks failed before the exchange), so kinds
+ * stay apart under the sum. */
 int wfpt_decode_result(const double r[3], double *out_logp);
 
 /* ---- measurement -------------------------------------------------------- */

@@ -68,6 +68,9 @@ def lib():
         L.oracle_wiener_like_multi.argtypes = [_PD, _I64, ctypes.POINTER(_PD), _PD, _D, _I, _I,
                                                _I, _D, _D, _D]
         L.oracle_count_evals.restype = _I64
+        L.oracle_wiener_like_multi_terms.restype = _D
+        L.oracle_wiener_like_multi_terms.argtypes = [_PD, _I64, ctypes.POINTER(_PD), _PD, _D, _I,
+                                                     _I, _I, _D, _D, _D, _PD]
         L.oracle_count_evals.argtypes = [_PD, _I64] + [_D] * 8 + [_I, _I, _I, _D]
         _lib = L
     return _lib
@@ -123,7 +126,9 @@ def pdf_array(x, v, sv, a, z, sz, t, st, err=1e-4, logp=0, n_st=2, n_sz=2, use_a
 
 
 def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=10,
-                      use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0):
+                      use_adaptive=1, simps_err=1e-3, p_outlier=0, w_outlier=0, terms=False):
+    """The reference's wiener_like_multi (wfpt.pyx:244-274); terms=True:
+    (sum, per-trial terms)."""
     x, px = _arr(x)
     vals = [v, sv, a, z, sz, t, st]
     names = ["v", "sv", "a", "z", "sz", "t", "st"]
@@ -140,8 +145,12 @@ def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=
         else:
             ptrs[j] = _PD()
             scal[j] = float(val)
-    return lib().oracle_wiener_like_multi(px, x.size, ptrs, scal, err, n_st, n_sz,
-                                          int(use_adaptive), simps_err, p_outlier, w_outlier)
+    out = np.empty(x.size) if terms else None
+    tot = lib().oracle_wiener_like_multi_terms(px, x.size, ptrs, scal, err, n_st, n_sz,
+                                               int(use_adaptive), simps_err, p_outlier,
+                                               w_outlier,
+                                               out.ctypes.data_as(_PD) if terms else None)
+    return (tot, out) if terms else tot
 
 
 def count_evals(x, v, sv, a, z, sz, t, st, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,

@@ -369,10 +369,11 @@ int oracle_pdf_array_omp(const double *x, int64_t n, double v, double sv, double
 }
 
 /* wfpt.pyx:244-274 */
-double oracle_wiener_like_multi(const double *x, int64_t n, const double *const arrays[7],
-                                const double scalars[7], double err, int n_st, int n_sz,
-                                int use_adaptive, double simps_err, double p_outlier,
-                                double w_outlier)
+/* wiener_like_multi with each trial's term of the sum in terms[i] (nullable) */
+double oracle_wiener_like_multi_terms(const double *x, int64_t n, const double *const arrays[7],
+                                      const double scalars[7], double err, int n_st, int n_sz,
+                                      int use_adaptive, double simps_err, double p_outlier,
+                                      double w_outlier, double *terms)
 {
     double sum_logp = 0;
     double wp_outlier = w_outlier * p_outlier;
@@ -390,9 +391,19 @@ double oracle_wiener_like_multi(const double *x, int64_t n, const double *const 
         } else {
             p = 1 - oracle_prob_ub(q[0], q[2], q[3]);
         }
+        if (terms) terms[i] = log(p);
         sum_logp += log(p);
     }
     return sum_logp;
+}
+
+double oracle_wiener_like_multi(const double *x, int64_t n, const double *const arrays[7],
+                                const double scalars[7], double err, int n_st, int n_sz,
+                                int use_adaptive, double simps_err, double p_outlier,
+                                double w_outlier)
+{
+    return oracle_wiener_like_multi_terms(x, n, arrays, scalars, err, n_st, n_sz, use_adaptive,
+                                          simps_err, p_outlier, w_outlier, NULL);
 }
 
 int64_t oracle_count_evals(const double *x, int64_t n, double v, double sv, double a, double z,

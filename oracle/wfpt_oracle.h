@@ -52,6 +52,10 @@ int oracle_pdf_array_omp(const double *x, int64_t n, double v, double sv, double
                          double w_outlier, double *out, int n_threads);
 /* wfpt.pyx:244-274 wiener_like_multi restated with per-trial parameter arrays
  * (any of v..st may be NULL => the scalar in `scalars` [v,sv,a,z,sz,t,st] is used). */
+double oracle_wiener_like_multi_terms(const double *x, int64_t n, const double *const arrays[7],
+                                      const double scalars[7], double err, int n_st, int n_sz,
+                                      int use_adaptive, double simps_err, double p_outlier,
+                                      double w_outlier, double *terms);
 double oracle_wiener_like_multi(const double *x, int64_t n, const double *const arrays[7],
                                 const double scalars[7], double err, int n_st, int n_sz,
                                 int use_adaptive, double simps_err, double p_outlier,

@@ -44,12 +44,21 @@ def _worker(rank, world, port, x, args, kn, inject, out_q):
     # this rank's {sum, zeros, encoded errors} triple, as finalize_kernel writes
     # it; the sum over ranks is what wfpt_wiener_like_allreduce's ncclAllReduce does
     err = inject.get(rank, 0.0)
-    t = torch.tensor([s, float(zeros), err], dtype=torch.float64)
+    if err == "fail":
+        # this rank's local pass failed: it still enters the exchange, with
+        # the library's poisoned triple (wfpt_wiener_like_allreduce does the
+        # same before its ncclAllReduce)
+        triple = _lib.poisoned_result()
+    else:
+        triple = [s, float(zeros), err]
+    t = torch.tensor(triple, dtype=torch.float64)
     dist.all_reduce(t)
     try:
         res = ("ok", _lib.decode_result(t.tolist()))  # the library's decode
     except NotImplementedError as e:
         res = ("error", str(e))
+    except _lib.CommError as e:
+        res = ("comm", str(e))
     out_q.put((rank, res, hi - lo))
     dist.barrier()
     dist.destroy_process_group()
@@ -158,3 +167,121 @@ def test_rccl_allreduce_call_sequences(gpu):
     for p in seq:
         got = ds.wiener_like_allreduce(*p, *kn)
         assert got == (ref_calm if p is calm else ref_heavy), p
+
+
+@pytest.mark.parametrize("inject", [{1: "fail"}, {0: "fail", 1: "fail"}, {0: "fail", 1: 1.0}])
+def test_two_rank_local_failure_before_exchange(inject):
+    """A rank whose local pass fails still enters the exchange with the
+    poisoned triple: every rank decodes an error (none waits in the
+    collective, none returns a number), the failed-rank count survives the
+    sum, and a depth error elsewhere is still reported next to it."""
+    rng = np.random.default_rng(7)
+    x = rng.choice([-1.0, 1.0], 400) * (0.35 + rng.gamma(2.0, 0.4, 400))
+    res = _run(x, (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0), (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1), inject)
+    nfail = sum(1 for v in inject.values() if v == "fail")
+    depth = any(v == 1.0 for v in inject.values())
+    for kind, msg in res:
+        assert kind == ("error" if depth else "comm"), (kind, msg)
+        assert f"{nfail} rank(s) failed before the likelihood exchange" in msg
+        assert ("WFPT_MAX_DEPTH" in msg) == depth
+
+
+_RDV_CHILD = r"""
+import sys, json
+sys.path.insert(0, sys.argv[1])
+from hddm_amd import dist as hdist
+rank, world, port, uid = int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), bytes.fromhex(sys.argv[5])
+got = hdist.exchange_id(rank, world, uid=uid if rank == 0 else None, host="127.0.0.1",
+                        port=port, timeout_s=60)
+print(json.dumps({"id": got.hex(), "torch": "torch" in sys.modules}))
+"""
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_tcp_rendezvous_hands_rank0_id_to_every_rank(world):
+    """The library's torch-free unique-id exchange (wfpt_comm_exchange_id,
+    used by wfpt_comm_init_tcp): every rank receives rank 0's 128 bytes, in
+    plain processes that never import torch."""
+    import json
+    import subprocess
+    import sys
+    port = _free_port()
+    uid = bytes(np.random.default_rng(world).integers(0, 256, 128, dtype=np.uint8))
+    procs = [subprocess.Popen([sys.executable, "-c", _RDV_CHILD, ROOT, str(r), str(world),
+                               str(port), uid.hex()], stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True)
+             for r in reversed(range(world))]  # peers first: they retry until rank 0 listens
+    outs = [p.communicate(timeout=120) for p in procs]
+    for p, (o, e) in zip(procs, outs):
+        assert p.returncode == 0, e
+        r = json.loads(o.strip().splitlines()[-1])
+        assert bytes.fromhex(r["id"]) == uid
+        assert r["torch"] is False
+
+
+def test_tcp_rendezvous_times_out_without_rank0():
+    """A peer whose rank 0 never shows up fails with an error naming the
+    rendezvous (no hang past its deadline)."""
+    from hddm_amd import _lib, dist as hdist
+    with pytest.raises(_lib.CommError, match="rendezvous"):
+        hdist.exchange_id(1, 2, host="127.0.0.1", port=_free_port(), timeout_s=0.5)
+
+
+def test_product_modules_do_not_import_torch():
+    """North_star: the product path has no PyTorch (the multi-GPU plumbing
+    included); bench.py and the tests may use it as harness."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import hddm_amd, hddm_amd.wfpt, hddm_amd.dist, hddm_amd.likelihoods, "
+            "hddm_amd.hierarchical, hddm_amd.integration, hddm_amd.cdfdif_wrapper\n"
+            "print('torch' in sys.modules)" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "False"
+
+
+@pytest.mark.gpu
+def test_rccl_local_failure_enters_exchange_and_recovers(gpu, monkeypatch):
+    """On the GPU through RCCL (world 1): a local failure (injected after the
+    local pass) still runs the collective with the poisoned triple and
+    returns the rank's own error; the communicator and the dataset stay usable
+    and the next call gives the local result bit for bit."""
+    from hddm_amd import _lib, dist as hdist
+    ctx = _lib.context()
+    hdist.init_comm(ctx, 0, 1)
+    rng = np.random.default_rng(8)
+    x = rng.choice([-1.0, 1.0], 20_000) * (0.35 + rng.gamma(2.0, 0.4, 20_000))
+    args = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    ds = gpu.Dataset(x)
+    ref = ds.wiener_like(*args, *kn)
+    monkeypatch.setenv("WFPT_FAULT", "allreduce_local")
+    with pytest.raises(RuntimeError, match="injected local failure"):
+        ds.wiener_like_allreduce(*args, *kn)
+    monkeypatch.delenv("WFPT_FAULT")
+    assert ds.wiener_like_allreduce(*args, *kn) == ref
+
+
+@pytest.mark.gpu
+def test_single_process_group_allreduce(gpu, oracle_lib):
+    """The single-process multi-GPU API (ncclCommInitAll + grouped
+    all-reduce) over the devices this box has: equals the
+    unsharded reference total."""
+    from hddm_amd import _lib, dist as hdist
+    nd = min(_lib.device_count(), 8)
+    grp = hdist.Group(list(range(nd)))
+    rng = np.random.default_rng(9)
+    x = rng.choice([-1.0, 1.0], 30_001) * (0.35 + rng.gamma(2.0, 0.4, 30_001))
+    args = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    shards = grp.shards(x)
+    assert sum(len(s) for s in shards) == x.size
+    ref = oracle_lib.pdf_array(x, *args, kn[0], 1, *kn[1:])
+    for _ in range(3):  # lean prediction from the second call on
+        got = grp.wiener_like(shards, *args, *kn)
+        assert abs(got - math.fsum(ref)) < 1e-11 * math.fsum(np.abs(ref))
+    x2 = x.copy()
+    x2[-1] = 0.1  # zero density on the last shard
+    assert grp.wiener_like(grp.shards(x2), *args, 1e-4, 2, 2, 1, 1e-3, 0.0, 0.1) == -math.inf

@@ -174,9 +174,9 @@ def test_call_sequence_determinism(gpu):
     assert a1 == a2 == a3 == a4, (a1, a2, a3, a4)
     assert b1 == b2, (b1, b2)
     # host-array path (full sequence) on the dataset's own trial order (a
-    # Dataset orders trials by |rt|; the chunk partials, and so the last bit
-    # of the total, follow the order)
-    xs = x[np.argsort(np.abs(x), kind="stable")]
+    # Dataset orders trials by boundary, then |rt|; the chunk partials, and so
+    # the last bit of the total, follow the order)
+    xs = x[np.lexsort((np.abs(x), x > 0))]
     host = gpu.wiener_like(xs, *defer, *kn)
     assert host == b1
 
