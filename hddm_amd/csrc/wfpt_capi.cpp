@@ -145,7 +145,7 @@ struct wfpt_ctx {
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
-  double* mres = nullptr;      // mapped pinned {sum, zeros, errors, deferred, word, heavy}
+  double* mres = nullptr;      // mapped pinned {sum, zeros, errors, deferred, word, heavy, #tree}
   double* mres_dev = nullptr;  // its device alias
   unsigned long long seq = 0;  // completion word finalize writes to mres[4]
   MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
@@ -154,6 +154,10 @@ struct wfpt_ctx {
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
+  // WFPT_LEAN_TREE: the largest fraction of refining chunks (last call) for
+  // which the lean pass + engine redo of those chunks beats the engine over
+  // every chunk
+  double lean_tree_max = 0.0;
   bool profile = false;      // HIP events around the main kernel
   bool count = false;        // pdf_sv evaluation counting
   double k_ms = 0.0;
@@ -179,6 +183,9 @@ struct wfpt_ds {
   // the last call on this dataset refined no chunk in-wave: the next one's
   // level-0 pass is the lean kernel (kPassLean)
   mutable bool no_tree = false;
+  // fraction of chunks that refined in-wave in the last call: up to
+  // lean_tree_max the lean pass still runs, the engine redoing those chunks
+  mutable double tree_frac = 1.0;
   bool input_order = false;  // WFPT_DS_INPUT_ORDER: trials kept in the caller's order
   // heavy-chunk record (wfpt_internal.h: Split), double-buffered by call
   // parity: the engine writes [1 - parity] while it reads [parity]
@@ -446,6 +453,17 @@ int read_sum(wfpt_ctx* c, const double* r, double* out, bool* deferred = nullptr
   return decode_sum(c, r, out, deferred);
 }
 
+// The dataset's in-wave refinement record from a finished call's result.
+void note_tree(const wfpt_ds* d, const double* r) {
+  d->no_tree = !res_tree(r);
+  d->tree_frac = d->nw > 0 ? r[6] / (double)d->nw : 0.0;
+}
+// The lean level-0 pass is predicted to pay: nothing refined last time, or
+// few enough chunks that their engine redo beats an engine pass over all.
+bool lean_predicted(const wfpt_ctx* c, const wfpt_ds* d) {
+  return c->lean && (d->no_tree || d->tree_frac <= c->lean_tree_max);
+}
+
 // Waits for a resident call, updates the dataset's predictions from its
 // result and decodes it.
 int finish_sum(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
@@ -457,7 +475,7 @@ int finish_sum(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt:
   const int rc = decode_sum(c, c->mres, out, &deferred);
   if (rc == WFPT_OK) {
     d->no_defer = c->fast_only && !deferred;
-    if (eng) d->no_tree = !res_tree(c->mres);
+    if (eng) note_tree(d, c->mres);
   }
   return rc;
 }
@@ -477,7 +495,7 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
   const int64_t n = d->n;
   if (c->count || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
   const bool eng = engine_family(P, K);
-  const bool lean = eng && c->lean && d->no_tree;
+  const bool lean = eng && lean_predicted(c, d);
   const bool fast = c->fast_only && d->no_defer;
   if (!lean && !fast) return -1;
   const int lp = lean ? wfpt::kPassLean : 0;
@@ -546,6 +564,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
+  if (const char* lt = std::getenv("WFPT_LEAN_TREE")) c->lean_tree_max = std::atof(lt);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -554,7 +573,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostMalloc((void**)&c->host_status, sizeof(int), hipHostMallocDefault);
   if (e == hipSuccess) e = hipMemset(c->status, 0, sizeof(int));
   if (e == hipSuccess)
-    e = hipHostMalloc((void**)&c->mres, 6 * sizeof(double),
+    e = hipHostMalloc((void**)&c->mres, 8 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
@@ -567,7 +586,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
     e = hipMalloc((void**)&c->phase, 8 * wfpt::kPhaseWaves * sizeof(unsigned long long));
   if (e == hipSuccess)
     e = hipMemset(c->phase, 0, 8 * wfpt::kPhaseWaves * sizeof(unsigned long long));
-  if (e == hipSuccess) std::memset(c->mres, 0, 6 * sizeof(double));
+  if (e == hipSuccess) std::memset(c->mres, 0, 8 * sizeof(double));
   if (e != hipSuccess) {
     wfpt_close(c);
     return fail(WFPT_ERR_HIP, std::string("wfpt_open: ") + hipGetErrorString(e));
@@ -1110,9 +1129,9 @@ struct ArState {
 };
 int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               ArState* st) {
-  HIP_TRY(c->res.reserve(6));
+  HIP_TRY(c->res.reserve(8));
   st->eng = engine_family(P, K);
-  st->lean = st->eng && c->lean && d->no_tree && !c->count;
+  st->lean = st->eng && lean_predicted(c, d) && !c->count;
   if (st->lean)
     return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d,
                    c->res.p);
@@ -1135,7 +1154,7 @@ int ar_finish(wfpt_ctx* c, const wfpt_ds* d, const ArState& st, double* out) {
   if (int rc = wait_result(c, c->mres)) return rc;
   split_advance(d, st.eng && !st.lean, c->mres);
   const int rc = decode_sum(c, c->mres, out);
-  if (rc == WFPT_OK && st.eng) d->no_tree = !res_tree(c->mres);
+  if (rc == WFPT_OK && st.eng) note_tree(d, c->mres);
   return rc;
 }
 }  // namespace

@@ -203,6 +203,7 @@ __device__ inline bool decide32(double tt, double err, Decision& D, float& args_
   const bool amb_b = fabsf(ksf - klf) <= tol * klf;
   const bool amb_k = fabsf(kk - rintf(kk)) <= tol * kk;
   if (Ll > -0.1f || Ls > -0.1f || amb_t || amb_l || amb_s || amb_b || amb_k) return false;
+  if (!(kk < 1e6f)) return false;  // huge / non-finite K: decide64's conversion
   D.small = ksf < klf;
   D.K = (int)ceilf(kk);
   D.amb = 0;
@@ -235,7 +236,7 @@ __device__ inline Decision decide64(double tt, double err) {
   Decision D;
   D.small = ks < kl;
   const double kk = D.small ? ks : kl;
-  D.K = (int)ceil(kk);
+  D.K = wfpt_x::ref_int(ceil(kk));  // the reference's x86 conversion
   constexpr double tol = 1e-12;
   D.amb = fabs(arg_l - 1.0) <= tol || fabs(arg_s - 1.0) <= tol || fabs(ks - kl) <= tol * kl ||
           fabs(kk - rint(kk)) <= tol * kk;
@@ -311,7 +312,7 @@ __device__ inline TNode tnode_setup(double xx, double v, double sv, double a, do
 #ifndef WFPT_SERIES_FMA
 #define WFPT_SERIES_FMA 1
 #endif
-__device__ inline double madd(double a, double b, double c) {
+__host__ __device__ inline double madd(double a, double b, double c) {
 #if WFPT_SERIES_FMA
   return fma(a, b, c);
 #else
@@ -319,7 +320,7 @@ __device__ inline double madd(double a, double b, double c) {
 #endif
 }
 // a b - c (the Chebyshev step 2cos(pi w) sin(k pi w) - sin((k-1) pi w))
-__device__ inline double msub(double a, double b, double c) {
+__host__ __device__ inline double msub(double a, double b, double c) {
 #if WFPT_SERIES_FMA
   return fma(a, b, -c);
 #else
@@ -874,31 +875,86 @@ __device__ inline ZGrid zgrid_setup(double lb, double ub, double v, double sv, d
 // (Chebyshev-node fit: max relative error 1.2e-16 in double Horner steps),
 // then ldexp, which also saturates to inf / 0 / subnormals for |x| > 709. No
 // special-case selects (OCML's exp carries them for inf / NaN arguments,
-// which these call sites never pass). WFPT_FAST_EXP=0 restores OCML's exp.
+// which the hot call sites never pass: their arguments are bounded by the
+// -600 / 600 guards around them; the rare sites use exp_sat). WFPT_FAST_EXP=0
+// restores OCML's exp.
 #ifndef WFPT_FAST_EXP
 #define WFPT_FAST_EXP 1
 #endif
+// One Horner step p r + c as a single three-operand v_fma_f64. Written with
+// fma(), the compiler selects the two-address v_fmac_f64 and, because the
+// coefficient c stays live for the next call site, copies it into the
+// accumulator first (a v_mov_b64 per step: 9 extra VALU instructions per
+// exponential). WFPT_HORNER_ASM=0 restores fma().
+#ifndef WFPT_HORNER_ASM
+#define WFPT_HORNER_ASM 1
+#endif
+__device__ inline double horner(double p, double r, double c) {
+#if WFPT_HORNER_ASM
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(p), "v"(r), "s"(c));
+  return d;
+#else
+  return fma(p, r, c);
+#endif
+}
+
 __device__ inline double exp_val(double x) {
 #if WFPT_FAST_EXP
   const double k = rint(x * 1.4426950408889634);
   double r = fma(-k, 6.9314718055994529e-01, x);
   r = fma(-k, 2.3190468138462996e-17, r);
   double p = 2.5110037605963777e-08;
-  p = fma(p, r, 2.763263963904103e-07);
-  p = fma(p, r, 2.755724091857897e-06);
-  p = fma(p, r, 2.4801485482328494e-05);
-  p = fma(p, r, 1.9841269890047113e-04);
-  p = fma(p, r, 1.3888888952314775e-03);
-  p = fma(p, r, 8.333333333319601e-03);
-  p = fma(p, r, 4.16666666664881e-02);
-  p = fma(p, r, 1.666666666666668e-01);
-  p = fma(p, r, 5.000000000000019e-01);
+  p = horner(p, r, 2.763263963904103e-07);
+  p = horner(p, r, 2.755724091857897e-06);
+  p = horner(p, r, 2.4801485482328494e-05);
+  p = horner(p, r, 1.9841269890047113e-04);
+  p = horner(p, r, 1.3888888952314775e-03);
+  p = horner(p, r, 8.333333333319601e-03);
+  p = horner(p, r, 4.16666666664881e-02);
+  p = horner(p, r, 1.666666666666668e-01);
+  p = horner(p, r, 5.000000000000019e-01);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
   return ldexp(p, (int)k);
 #else
   return exp(x);
 #endif
+}
+
+// Large-time sines of a grid (pdf.pxi:61-62: sin(k pi w) at the grid's 5
+// nodes), k = 1..kSinK, exactly as tnode_pdf_sv_grid5's recurrence produces
+// them: sin / cos of nodes 1..3 rotated from node 0 (node 4 direct), then
+// s_k = 2 cos(pi w) s_{k-1} - s_{k-2} in the same fused operations. Built on
+// the host per call (RootGrids) so the lean pass reads them instead of
+// recomputing them per lane; bit-identical to the per-lane recurrence.
+constexpr int kSinK = 8;
+__host__ __device__ inline void sin_rot(const ZGrid& G, double (&sj)[5], double (&cj)[5]) {
+  sj[0] = G.s0;
+  cj[0] = G.c0;
+  sj[4] = G.s4;
+  cj[4] = G.c4;
+  for (int j = 1; j < 4; ++j) {
+    sj[j] = fma(sj[j - 1], G.cd, cj[j - 1] * G.sd);
+    cj[j] = fma(cj[j - 1], G.cd, -(sj[j - 1] * G.sd));
+  }
+}
+// 2 cos(pi g_i) of node i (the recurrence's multiplier)
+__host__ __device__ inline double sin_tc(const ZGrid& G, int i) {
+  double sj[5], cj[5];
+  sin_rot(G, sj, cj);
+  const double c = i == 0 ? cj[0] : i == 1 ? cj[1] : i == 2 ? cj[2] : i == 3 ? cj[3] : cj[4];
+  return c + c;
+}
+__host__ __device__ inline void sin_table(const ZGrid& G, double (&S)[kSinK + 1][5]) {
+  double sj[5], cj[5];
+  sin_rot(G, sj, cj);
+  for (int i = 0; i < 5; ++i) {
+    const double tc = cj[i] + cj[i];
+    S[0][i] = 0.0;
+    S[1][i] = sj[i];
+    for (int k = 2; k <= kSinK; ++k) S[k][i] = msub(tc, S[k - 1][i], S[k - 2][i]);
+  }
 }
 
 // Element i (a run-time index) of a 5-element register array, and its store:
@@ -918,6 +974,12 @@ __device__ inline void put5(double (&v)[5], int i, double x) {
   v[4] = i == 4 ? x : v[4];
 }
 
+// The rare paths' exponentials, whose arguments can be infinite (|v| ~ 1e154
+// makes v^2 x overflow; a subnormal tt makes the exponent multiplier
+// overflow): libm's exp, which gives 0 for -inf like the reference
+// (exp_val's range reduction would make NaN of it).
+__device__ inline double exp_sat(double x) { return exp(x); }
+
 // pdf_sv at the 5 root-level z nodes of one t node (the values of
 // tnode_pdf_sv at each node to a few ulp):
 //   * small-t series: the exponents (g_j + 2k)^2 m are quadratic in j on the
@@ -927,8 +989,12 @@ __device__ inline void put5(double (&v)[5], int i, double x) {
 //   * large-t series: the Chebyshev recurrence in k from the rotated sin/cos;
 //   * the drift factor exp(c_j): three exponentials and the second-difference
 //     recurrence (direct exps when |c| > 600).
+// stab (nullable): the grid's large-time sine table sin(k pi g_i), row k at
+// stab + 5 k (k = 1..kSinK; SinTable); null: the Chebyshev recurrence in
+// registers.
 __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
-                                          double a, double (&out)[5]) {
+                                          double a, double (&out)[5],
+                                          const double* stab = nullptr) {
   double p[5];
 #pragma unroll
   for (int i = 0; i < 5; ++i) p[i] = 0.0;
@@ -973,12 +1039,50 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 #pragma unroll 1
         for (int i = 0; i < 5; ++i) {
           const double wi = pick5(G.g, i) + k2;
-          put5(p, i, madd(wi, exp_val((wi * wi) * T.m), pick5(p, i)));
+          put5(p, i, madd(wi, exp_sat((wi * wi) * T.m), pick5(p, i)));
         }
       }
     }
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = p[i] * T.rn;
+  } else if (stab) {
+    // the sines of the (wave-uniform) grid from the call's table: the same
+    // values the recurrence below produces (sin_table), read with scalar
+    // loads instead of carried in 15 vector registers per lane
+    double e = T.m, r = T.m * T.q2;
+    if (K >= 1) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) p[i] = T.m * stab[5 + i];
+    }
+    if (K <= kSinK) {
+      for (int k = 2; k <= K; ++k) {
+        e = e * r;
+        r = r * T.q2;
+        const double ke = (double)k * e;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) p[i] = madd(ke, stab[5 * k + i], p[i]);
+      }
+    } else {
+      // beyond the table (err far below 1e-10): the recurrence one node at
+      // a time (few live registers)
+#pragma unroll 1
+      for (int i = 0; i < 5; ++i) {
+        const double s1 = stab[5 + i];
+        const double tci = sin_tc(G, i);
+        double e1 = T.m, r1 = T.m * T.q2, sk = s1, skm1 = 0.0, pi = T.m * s1;
+        for (int k = 2; k <= K; ++k) {
+          e1 = e1 * r1;
+          r1 = r1 * T.q2;
+          const double sn = msub(tci, sk, skm1);
+          skm1 = sk;
+          sk = sn;
+          pi = madd((double)k * e1, sk, pi);
+        }
+        put5(p, i, pi);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; ++i) p[i] = p[i] * kPi;
   } else {
     double sj[5], cj[5];
     sj[0] = G.s0;
@@ -1050,7 +1154,7 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 #pragma unroll 1
     for (int i = 0; i < 5; ++i) {
       const double Ai = pick5(G.A, i);
-      put5(ex, i, exp_val((sv == 0) ? Ai - (T.vvx * 0.5) : (Ai - T.vvx) * T.cden));
+      put5(ex, i, exp_sat((sv == 0) ? Ai - (T.vvx * 0.5) : (Ai - T.vvx) * T.cden));
     }
   }
   // the common case: every series value positive and every product finite;
@@ -1133,9 +1237,10 @@ __device__ inline double simp_value(const Simp& s) { return s.S2 + (s.S2 - s.S) 
 // root estimate; the caller defers the trial).
 __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, double v,
                                     double sv, double a, const Knobs& K, int& flags,
-                                    long long& ne, bool& repair) {
+                                    long long& ne, bool& repair,
+                                    const double* stab = nullptr) {
   double f[5];
-  if (!tnode_pdf_sv_grid5(T, G, v, sv, a, f)) flags |= kFlagExact;
+  if (!tnode_pdf_sv_grid5(T, G, v, sv, a, f, stab)) flags |= kFlagExact;
 #pragma unroll
   for (int i = 0; i < 5; ++i) f[i] = f[i] * iZz;
   ne += 5;
@@ -1205,6 +1310,9 @@ struct L0Hints {
   double ia2;  // 1 / a^2
   Decision D0, D4;
   bool ok0, ok4, shared;
+  __device__ double qh(int j) const {
+    return j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
+  }
 };
 __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, double err) {
   L0Hints H;
@@ -1242,15 +1350,14 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
 template <int MODE>
 __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& K, double lb,
                                  double ub, const L0Hints& H, int j, const ZGrid& G, int& flags,
-                                 bool& pend, long long& ne) {
+                                 bool& pend, long long& ne, const double* stab = nullptr) {
   const double a = P.a, sv = P.sv, err = K.err;
   const double x = tr.x, v = tr.v, z = tr.z;
   const double iw = 1.0 / (ub - lb);
   const double c = (ub + lb) / 2.;
   const double d = (lb + c) / 2., e = (c + ub) / 2.;
   const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
-  const double qh =
-      j == 0 ? H.qn[0] : j == 1 ? H.qn[1] : j == 2 ? H.qn[2] : j == 3 ? H.qn[3] : H.qn[4];
+  const double qh = H.qh(j);
   const bool known = j == 0 ? H.ok0 : (j == 4 ? H.ok4 : H.shared);
   const TNode T = tnode_setup_r(x - tc, v, sv, a, H.ia2, err, qh, known, j == 4 ? H.D4 : H.D0);
   pend = false;
@@ -1260,7 +1367,7 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
   }
   if (MODE == kAdaptTZ) {
     const double iZz = 1.0 / ((z + tr.sz / 2.) - (z - tr.sz / 2.));
-    return inner_root(T, G, iZz, v, sv, a, K, flags, ne, pend) * iw;
+    return inner_root(T, G, iZz, v, sv, a, K, flags, ne, pend, stab) * iw;
   }
   ne += 1;
   return tnode_pdf_sv(T, z, v, sv, a) * iw;
@@ -1271,7 +1378,7 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
 template <int MODE>
 __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs& K,
                                    const ZGrid& G, double& p, double (&f)[5], long long& ne,
-                                   unsigned& pend) {
+                                   unsigned& pend, const double* stab = nullptr) {
   p = 0.0;
   pend = 0u;
   if (!tr.valid) return kFinal;
@@ -1282,7 +1389,7 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
     const double iw = 1.0 / (ub - lb);
     const TNode T = tnode_setup(tr.x - P.t, tr.v, P.sv, P.a, K.err);
     if (T.amb) return kExact;
-    if (!tnode_pdf_sv_grid5(T, G, tr.v, P.sv, P.a, f)) return kExact;
+    if (!tnode_pdf_sv_grid5(T, G, tr.v, P.sv, P.a, f, stab)) return kExact;
 #pragma unroll
     for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
     ne += 5;
@@ -1291,7 +1398,7 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
 #pragma unroll 1
     for (int j = 0; j < 5; ++j) {
       bool pj;
-      const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne);
+      const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);
       if (flags & kFlagExact) return kExact;
       if (pj) pend |= 1u << (j * (kTreeW / 4));
       if (j == 0) f[0] = y;
@@ -1455,11 +1562,13 @@ __host__ __device__ inline void eng_tables(const Params& P, EngTables& T) {
 // same zgrid_of calls as eng_tables' G[flip][kGridRoot], so bit-identical.
 struct RootGrids {
   ZGrid G[2];
+  double S[2][kSinK + 1][5];  // their large-time sine tables (sin_table)
 };
 __host__ __device__ inline void root_grids(const Params& P, RootGrids& R) {
   for (int flip = 0; flip < 2; ++flip) {
     const double zf = flip ? 1. - P.z : P.z, vf = flip ? -P.v : P.v;
     R.G[flip] = zgrid_of(zf - P.sz / 2., zf + P.sz / 2., kGridRoot, vf, P.sv, P.a);
+    sin_table(R.G[flip], R.S[flip]);
   }
 }
 

@@ -29,6 +29,15 @@ constexpr double kPi2 = kPi * kPi;
 constexpr int kMaxDepth = 24;              // WFPT_MAX_DEPTH
 constexpr long long kEvalBudget = 1ll << 24;  // WFPT_EVAL_BUDGET
 
+// <int>(double) as the reference's x86-64 build converts (cvttsd2si): a value
+// outside int's range, inf or NaN gives INT_MIN (the "integer indefinite"),
+// where gfx950's conversion saturates. A non-finite term count (tt = 0 from
+// an overflowing a, err = 0) thus runs no series term, as in the reference,
+// instead of ~2^31 of them.
+WFPT_HD int ref_int(double v) {
+  return (v < 2147483648.0 && v > -2147483649.0) ? (int)v : (-2147483647 - 1);
+}
+
 // pdf.pxi:28-65
 WFPT_HD double ftt_01w(double tt, double w, double err) {
   double kl, ks, p;
@@ -48,16 +57,16 @@ WFPT_HD double ftt_01w(double tt, double w, double err) {
   }
   p = 0.0;
   if (ks < kl) {
-    const int K = (int)ceil(ks);
-    const int lower = (int)(-floor((K - 1) / 2.));
-    const int upper = (int)ceil((K - 1) / 2.);
+    const int K = ref_int(ceil(ks));
+    const int lower = ref_int(-floor((K - 1) / 2.));
+    const int upper = ref_int(ceil((K - 1) / 2.));
     for (int k = lower; k <= upper; ++k) {
       const double wk = w + (double)(2 * k);
       p = p + wk * cr_exp(((-(wk * wk)) / 2.0) / tt);
     }
     p = p / sqrt((2.0 * kPi) * cr_cube(tt));
   } else {
-    const int K = (int)ceil(kl);
+    const int K = ref_int(ceil(kl));
     for (int k = 1; k <= K; ++k) {
       const double dk = (double)k;
       p = p + (dk * cr_exp((((-(dk * dk)) * kPi2) * tt) / 2.0)) * cr_sin((dk * kPi) * w);

@@ -87,7 +87,8 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
                    const Split* split = nullptr);
 // out[0..3] = {sum of nb partials, #zero trials, encoded error flags,
 // kResDeferred (defer_bits: some chunk's zero word carries kZeroDefer) |
-// kResTree (*tree_any; then *tree_any = 0)}, out[5] = *split_rd (the heavy chunks the call
+// kResTree (*tree_any; then *tree_any = 0)}, out[6] = *tree_any (chunks that
+// refined in-wave), out[5] = *split_rd (the heavy chunks the call
 // recorded, or 0; then *split_rs = 0), then out[4] = seq (a 64-bit word) once
 // they are visible; resets *status to 0. mirror (optional, device memory):
 // out[0..3] and out[5] written there too.

@@ -424,7 +424,7 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
       if (MODE != kAdaptZ && L == 0 && stage == 0) {
         const L0Hints H = l0_hints(xa, cl.tab.tP[0], cl.tab.tP[kTreeW], a, err);
         const int j = pos / (kTreeW / 4);
-        qh = j == 0 ? H.qn[0] : j == 1 ? H.qn[1] : j == 2 ? H.qn[2] : j == 3 ? H.qn[3] : H.qn[4];
+        qh = H.qh(j);
         known = j == 0 ? H.ok0 : (j == 4 ? H.ok4 : H.shared);
         kd = j == 4 ? H.D4 : H.D0;
       }
@@ -704,7 +704,9 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
   Tally ty;
   int nz0 = 0;
   if (rounds) {
-    if (lane == 0) *W.tree_any = 1;  // same-value plain stores: no atomic
+    // chunks that refined in-wave (a split chunk once: its unit 0); finalize
+    // reports the count, which picks the next call's level-0 pass
+    if (lane == 0 && (!split || sub == 0)) atomicAdd(W.tree_any, 1);
     wave_sync();
     nz0 = cl.qn[1];
     pc.mark(1);
@@ -769,6 +771,12 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
   return G;
 }
 
+// WFPT_SIN_TABLE=0: the lean pass evaluates the large-time sines per lane
+// (the recurrence) instead of reading the call's table (same values).
+#ifndef WFPT_SIN_TABLE
+#define WFPT_SIN_TABLE 1
+#endif
+
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
@@ -793,10 +801,11 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const int b = (bp == bo) ? 1 : 0;  // every trial upper: 1; otherwise lower first
   if (own && pos == (b != 0))
     oc = eng_level0_t<MODE>(trial_setup_b(x0, A.P, b != 0), A.P, A.K, zgrid_uniform(R, b), p,
-                            f0, ne0, pend0);
+                            f0, ne0, pend0, WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
   if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
     if (own && pos)
-      oc = eng_level0_t<MODE>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0, ne0, pend0);
+      oc = eng_level0_t<MODE>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0, ne0, pend0,
+                              WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
   }
   if (__ballot(oc == kTree) != 0ull) {
     if (lane == 0) {
@@ -1055,10 +1064,13 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
     out[1] = (double)zz;
     out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
     int res3 = dd ? kResDeferred : 0;
+    double ntree = 0.0;
     if (tree_any) {
       if (*tree_any) res3 |= kResTree;
+      ntree = (double)*tree_any;
       *tree_any = 0;
     }
+    out[6] = ntree;
     out[3] = (double)res3;
     // heavy chunks recorded for the next call (Split)
     out[5] = split_rd ? (double)*split_rd : 0.0;
@@ -1069,6 +1081,7 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
       mirror[2] = out[2];
       mirror[3] = out[3];
       mirror[5] = out[5];
+      mirror[6] = out[6];
     }
     __threadfence_system();
     // completion word, written after the results are visible: the host may
@@ -1088,6 +1101,7 @@ __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* 
     out[2] = res[2];
     out[3] = res[3];
     out[5] = res[5];
+    out[6] = res[6];
     __threadfence_system();
     reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
     __threadfence_system();

@@ -38,22 +38,30 @@ class _ResidentCache:
     """Device-resident copies of node data (a node's RT column never changes
     during sampling; changed data is a new entry).
 
-    A logp call must not pay an O(n) host pass in front of a ~0.15 ms kernel,
-    so lookups are keyed on the column's identity (buffer address, length and
-    the node's value object, which the entry keeps alive so neither can be
+    Lookups are keyed on the column's identity (buffer address, length and the
+    node's value object, which the entry keeps alive so neither can be
     recycled while the entry exists). Contents are hashed only on a miss (nodes
-    holding equal data share one upload); a hit re-checks a 64-element sample
-    of the column so an in-place rewrite of a node's value is not served stale.
+    holding equal data share one upload). A hit re-checks the column against
+    the entry: exactly (every element) for columns of up to EXACT_MAX trials —
+    HDDM's nodes, where the compare is ~1 us — so an in-place rewrite of a
+    node's value is never served stale; larger columns, whose full compare
+    would cost more than their kernel, are re-checked on a 256-element sample
+    only (an in-place rewrite missing every sampled element is not detected:
+    pass a new array instead of rewriting one).
     Each entry also caches max|rt| for wfpt_like's `< 998` dispatch."""
+
+    EXACT_MAX = 16384
 
     def __init__(self, maxsize=4096):
         self._by_id = {}
         self._by_bytes = {}
         self.maxsize = maxsize
 
-    @staticmethod
-    def _probe(rt):
-        return rt[:: max(1, rt.size // 64)][:64].copy()
+    @classmethod
+    def _probe(cls, rt):
+        if rt.size <= cls.EXACT_MAX:
+            return rt.copy()
+        return rt[:: max(1, rt.size // 256)][:256].copy()
 
     def get(self, rt, src):
         """(Dataset or None, max|rt|) for the contiguous column `rt` of `src`.

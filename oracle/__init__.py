@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIBDIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIBDIR, "liboracle_wfpt.so")
 SRC = os.path.join(HERE, "wfpt_oracle.c")
+SRC_CDF = os.path.join(HERE, "cdfdif_oracle.c")
 
 _D = ctypes.c_double
 _I = ctypes.c_int
@@ -32,11 +33,11 @@ def build(force=False):
     """gcc -O2 -ffp-contract=off (the reference's setup.py:4-7 uses -O2, no FMA)."""
     os.makedirs(LIBDIR, exist_ok=True)
     hdr = os.path.join(HERE, "wfpt_oracle.h")
-    if (not force and os.path.exists(LIB) and os.path.getmtime(LIB) > os.path.getmtime(SRC)
-            and os.path.getmtime(LIB) > os.path.getmtime(hdr)):
+    if (not force and os.path.exists(LIB)
+            and all(os.path.getmtime(LIB) > os.path.getmtime(f) for f in (SRC, SRC_CDF, hdr))):
         return LIB
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-fPIC",
-                    "-shared", "-o", LIB, SRC, "-lm"], check=True)
+                    "-shared", "-o", LIB, SRC, SRC_CDF, "-lm"], check=True)
     return LIB
 
 
@@ -72,6 +73,10 @@ def lib():
         L.oracle_wiener_like_multi_terms.argtypes = [_PD, _I64, ctypes.POINTER(_PD), _PD, _D, _I,
                                                      _I, _I, _D, _D, _D, _PD]
         L.oracle_count_evals.argtypes = [_PD, _I64] + [_D] * 8 + [_I, _I, _I, _D]
+        L.oracle_dmat_cdf_array.restype = _I
+        L.oracle_dmat_cdf_array.argtypes = [_PD, _I64] + [_D] * 9 + [_PD]
+        L.oracle_dmat_cdf_array_omp.restype = _I
+        L.oracle_dmat_cdf_array_omp.argtypes = [_PD, _I64] + [_D] * 9 + [_PD, _I]
         _lib = L
     return _lib
 
@@ -151,6 +156,22 @@ def wiener_like_multi(x, v, sv, a, z, sz, t, st, err, multi=None, n_st=10, n_sz=
                                                w_outlier,
                                                out.ctypes.data_as(_PD) if terms else None)
     return (tot, out) if terms else tot
+
+
+def dmat_cdf_array(x, v, sv, a, z, sz, t, st, p_outlier, w_outlier, n_threads=None):
+    """The reference's cdfdif_wrapper.dmat_cdf_array (cdfdif_wrapper.pyx:16-53
+    over cdfdif.c:59-221) restated in C (oracle/cdfdif_oracle.c)."""
+    x, px = _arr(x)
+    out = np.empty_like(x)
+    if n_threads is None:
+        rc = lib().oracle_dmat_cdf_array(px, x.size, v, sv, a, z, sz, t, st, p_outlier,
+                                         w_outlier, out.ctypes.data_as(_PD))
+    else:
+        rc = lib().oracle_dmat_cdf_array_omp(px, x.size, v, sv, a, z, sz, t, st, p_outlier,
+                                             w_outlier, out.ctypes.data_as(_PD), int(n_threads))
+    if rc < 0:
+        raise ValueError("at least one of the parameters is out of the support")
+    return out
 
 
 def count_evals(x, v, sv, a, z, sz, t, st, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,

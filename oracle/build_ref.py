@@ -4,8 +4,9 @@ Recipe that compiles the reference's own WFPT kernels (src/pdf.pxi +
 src/integrate.pxi, read where they lie under /root/reference) into
 oracle/_ref/ref_shim<EXT_SUFFIX>. Outputs go only into oracle/_ref/ (git-ignored).
 
-Mirrors the reference build of setup.py:4-7 (Cython -> C++, g++ -O2, no
--fopenmp). Cython's `include "integrate.pxi"` is resolved through the
+Mirrors the reference build of setup.py:4-7 (Cython -> C++, g++ -O2); the one
+addition, -fopenmp, only parallelises the shim's pdf_array_prange (the
+all-threads CPU calibration), not the reference's own loops. Cython's `include "integrate.pxi"` is resolved through the
 include path, so nothing from the reference is copied into this repository.
 
 Usage:  python oracle/build_ref.py [--reference /root/reference]
@@ -36,7 +37,9 @@ def build(reference="/root/reference", quiet=False):
     run = (lambda c: subprocess.run(c, check=True, stdout=subprocess.DEVNULL)) if quiet else \
         (lambda c: subprocess.run(c, check=True))
     run([sys.executable, "-m", "cython", "--cplus", "-2", "-I", src, "-o", cpp, pyx])
-    run(["g++", "-O2", "-fwrapv", "-fPIC", "-DNDEBUG", "-shared",
+    # -fopenmp only parallelises pdf_array_prange (the all-threads calibration
+    # row); every kernel and the serial loops compile as with setup.py:4-7
+    run(["g++", "-O2", "-fwrapv", "-fPIC", "-DNDEBUG", "-shared", "-fopenmp",
          "-DNPY_NO_DEPRECATED_API=NPY_1_7_API_VERSION",
          "-I", sysconfig.get_paths()["include"], "-I", np.get_include(),
          cpp, "-o", so])

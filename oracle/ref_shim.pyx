@@ -44,6 +44,25 @@ def pdf_array(np.ndarray[double, ndim=1] x, double v, double sv, double a, doubl
         return np.log(y)
     return y
 
+# wfpt.pyx:32-42's prange loop around the reference full_pdf, for the
+# all-threads CPU calibration only: oracle/build_ref.py compiles this module
+# with -fopenmp so the prange runs in parallel (the reference's own setup.py
+# has no -fopenmp, so its pdf_array runs serially). Densities only (no
+# mixture / log epilogue): the same loop shape as oracle_pdf_array_omp.
+from cython.parallel import prange
+
+def pdf_array_prange(np.ndarray[double, ndim=1] x, double v, double sv, double a, double z,
+                     double sz, double t, double st, double err=1e-4, int n_st=2, int n_sz=2,
+                     bint use_adaptive=1, double simps_err=1e-3, int n_threads=1):
+    cdef Py_ssize_t size = x.shape[0]
+    cdef Py_ssize_t i
+    cdef np.ndarray[double, ndim=1] y = np.empty(size, dtype=np.double)
+    cdef double[::1] yv = y
+    cdef double[::1] xv = x
+    for i in prange(size, nogil=True, num_threads=n_threads, schedule='static'):
+        yv[i] = full_pdf(xv[i], v, sv, a, z, sz, t, st, err, n_st, n_sz, use_adaptive, simps_err)
+    return y
+
 # restatement of wfpt.pyx:54-76 around the reference full_pdf
 def wiener_like(np.ndarray[double, ndim=1] x, double v, double sv, double a, double z, double sz, double t,
                 double st, double err, int n_st=10, int n_sz=10, bint use_adaptive=1, double simps_err=1e-8,

@@ -15,8 +15,12 @@ accurate there. The bar is therefore |dF| <= CDF_ATOL where sz and st are
 both >= 0.05 (well conditioned) and |dF| <= CDF_ATOL_ILL otherwise
 (measured on MI355X: max |dF| = 1.4e-8 over the golden set).
 """
+import os
+
 import numpy as np
 import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CDF_ATOL = 1e-9
 CDF_ATOL_ILL = 1e-6
@@ -133,3 +137,39 @@ def test_stochastic_cdf_hook():
     node = cls("wfpt", np.array([0.5, -0.8]), v=v, sv=sv, a=a, z=z, sz=sz, t=t, st=st,
                p_outlier=po)
     np.testing.assert_allclose(node.cdf(g["hook_x"]), g["hook_y"], atol=CDF_ATOL)
+
+
+def test_cdf_oracle_bit_exact_on_reference_fixtures(oracle_lib):
+    """oracle/cdfdif_oracle.c (the C restatement that times the CDF row's CPU
+    baseline on the GPU box) gives the reference's doubles on every fixture
+    generated by the reference's own cdfdif_wrapper (tests/golden/cdfdif*.npz),
+    and agrees with that extension directly when it is built (oracle/_ref)."""
+    n = 0
+    for fn in ("cdfdif", "cdfdif_random"):
+        g = np.load(os.path.join(ROOT, "tests", "golden", fn + ".npz"), allow_pickle=False)
+        for p, x, y in zip(g["params"], g["x"], g["y"]):
+            got = oracle_lib.dmat_cdf_array(x, *p)
+            assert np.array_equal(got, y, equal_nan=True), (fn, p)
+            n += x.size
+        if "hook_params" in g.files:
+            got = oracle_lib.dmat_cdf_array(g["hook_x"], *g["hook_params"])
+            assert np.array_equal(got, g["hook_y"])
+    assert n > 20000
+    # the multi-thread version is the same per-trial computation
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cdfdif_random.npz"), allow_pickle=False)
+    p, x = g["params"][0], g["x"][0]
+    assert np.array_equal(oracle_lib.dmat_cdf_array(x, *p, n_threads=4),
+                          oracle_lib.dmat_cdf_array(x, *p))
+    with pytest.raises(ValueError):
+        oracle_lib.dmat_cdf_array(x, 0.5, 0.1, -1.0, 0.5, 0.1, 0.3, 0.1, 0.0, 0.1)
+    import oracle
+    R = oracle.load_ref_cdfdif()
+    if R is not None:
+        rng = np.random.default_rng(3)
+        for _ in range(5):
+            p = (rng.uniform(-3, 3), rng.uniform(0, 2), rng.uniform(0.6, 2.5),
+                 rng.uniform(0.35, 0.65), rng.uniform(0.0, 0.3), rng.uniform(0.2, 0.5),
+                 rng.uniform(0.0, 0.3), 0.0, 0.1)
+            x = rng.choice([-1.0, 1.0], 300) * rng.uniform(0.05, 3.0, 300)
+            assert np.array_equal(oracle_lib.dmat_cdf_array(x, *p),
+                                  R.dmat_cdf_array(x, *p), equal_nan=True), p

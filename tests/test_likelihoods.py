@@ -66,6 +66,14 @@ def test_resident_cache_identity_and_staleness(gpu, oracle_lib):
     c = like(df, *args, p_outlier=0.05)
     ref2 = oracle_lib.wiener_like(df["rt"].to_numpy(), *args, *kn)
     assert abs(c - ref2) < 1e-9 * abs(ref2) and c != a
+    # one element that no sample would cover (the column is below EXACT_MAX:
+    # the whole column is compared on every hit)
+    col = df["rt"].to_numpy()
+    col[57] = col[57] * 1.05
+    df["rt"] = col
+    d = like(df, *args, p_outlier=0.05)
+    ref3 = oracle_lib.wiener_like(df["rt"].to_numpy(), *args, *kn)
+    assert abs(d - ref3) < 1e-9 * abs(ref3) and d != c
     # a second node holding equal data shares the upload
     n0 = len(likelihoods._cache._by_bytes)
     like(pd.DataFrame({"rt": df["rt"].to_numpy().copy()}), *args, p_outlier=0.05)

@@ -337,3 +337,32 @@ def test_shared_decision_grid_straddling_ks_peak(gpu, oracle_lib):
             tot = ds.wiener_like(*args, 2, 2, 1, 1e-3, 0.05, 0.1)
             terms = oracle_lib.pdf_array(x, *args, 1, 2, 2, 1, 1e-3, 0.05, 0.1)
             assert abs(tot - math.fsum(terms)) <= 1e-11 * math.fsum(np.abs(terms))
+
+
+@pytest.mark.parametrize("p", [
+    (1e160, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0), (-1e160, 0.5, 2.0, 0.5, 0.1, 0.3, 0.1),
+    (3e77, 0.3, 2.0, 0.5, 0.1, 0.3, 0.1), (0.5, 1e160, 2.0, 0.5, 0.1, 0.3, 0.1),
+    (0.5, 0.1, 1e160, 0.5, 0.1, 0.3, 0.1), (0.5, 0.1, 1e-160, 0.5, 0.1, 0.3, 0.1),
+    (40.0, 2.5, 0.5, 0.5, 0.1, 0.3, 0.1), (-40.0, 0.0, 0.5, 0.5, 0.0, 0.3, 0.0)])
+def test_extreme_parameters_match_reference(gpu, oracle_lib, p):
+    """Parameters that overflow / underflow the series and drift exponents
+    (-inf arguments of the fitted exp): per-trial densities and
+    log mixtures with and without outliers, and resident totals, follow the
+    reference's semantics (0, -inf, NaN exactly where it gives them)."""
+    from test_gpu_parity import assert_density_parity
+    rng = np.random.default_rng(41)
+    x = rng.choice([-1.0, 1.0], 512) * (0.3 + rng.gamma(2.0, 0.4, 512))
+    x[:8] = [0.30001, -0.30001, 0.3 + 1e-9, 0.0, 1e-300, 5.0, -5.0, 0.25]
+    for po, w in ((0.0, 0.0), (0.05, 0.1)):
+        ref = oracle_lib.pdf_array(x, *p, 1e-4, 0, 2, 2, 1, 1e-3, po, w)
+        got = gpu.pdf_array(x, *p, 1e-4, 0, 2, 2, 1, 1e-3, po, w)
+        assert_density_parity(got, ref, f"{p} po={po}")
+        ds = gpu.Dataset(x)
+        want = oracle_lib.wiener_like(x, *p, 1e-4, 2, 2, 1, 1e-3, po, w)
+        for _ in range(2):  # full sequence, then the predicted (lean) one
+            tot = ds.wiener_like(*p, 1e-4, 2, 2, 1, 1e-3, po, w)
+            if np.isnan(want) or np.isinf(want):
+                assert (np.isnan(tot) and np.isnan(want)) or tot == want, (p, po, tot, want)
+            else:
+                terms = oracle_lib.pdf_array(x, *p, 1e-4, 1, 2, 2, 1, 1e-3, po, w)
+                assert abs(tot - math.fsum(terms)) <= 1e-11 * math.fsum(np.abs(terms)), (p, po)

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "w3": ["WFPT_FAST_WAVES_TZ=3"],
+    "noasm": ["WFPT_HORNER_ASM=0"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 

@@ -32,13 +32,19 @@ def main():
     ap.add_argument("--full", action="store_true", help="include sv, sz, st (full DDM)")
     ap.add_argument("--progress", type=int, default=0)
     ap.add_argument("--json", default=None, help="also write the JSON line here")
+    ap.add_argument("--dt", type=float, default=1e-4,
+                    help="RT grid of the data sampler (the reference's sampling_dt default "
+                         "is 1e-4, hddm/likelihoods.py:30)")
+    ap.add_argument("--seed", type=int, default=20261017)
+    ap.add_argument("--sv", type=float, default=0.1, help="true sv with --full")
     a = ap.parse_args()
     from hddm_amd.hierarchical import HDDM, gen_data
     t0 = time.perf_counter()
     sv = sz = st = 0.0
     if a.full:
-        sv, sz, st = 0.1, 0.1, 0.1
-    data, truth = gen_data(n_subj=a.subjects, n_trials=a.trials, sv=sv, sz=sz, st=st)
+        sv, sz, st = a.sv, 0.1, 0.1
+    data, truth = gen_data(n_subj=a.subjects, n_trials=a.trials, sv=sv, sz=sz, st=st,
+                           seed=a.seed, dt=a.dt)
     t_gen = time.perf_counter() - t0
     m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st") if a.full else (),
              seed=1)
@@ -57,7 +63,7 @@ def main():
         "value": a.iters / el, "unit": "sweeps/s",
         "config": {"subjects": a.subjects, "trials_per_subject": a.trials,
                    "nodes": m.n_nodes, "trials": m.n_trials, "full_ddm": a.full,
-                   "iters": a.iters},
+                   "iters": a.iters, "data_dt": a.dt, "seed": a.seed},
         "seconds": el, "extrapolated_sample_2000_s": 2000 * el / a.iters,
         "batched_likelihood_calls_per_sweep": calls / a.iters,
         "likelihood_fraction_of_time": lik_s / el,

@@ -56,6 +56,11 @@ def cpu_rate(fn, n, budget):
             return n * reps / el
 
 
+def threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() else len(os.sched_getaffinity(0))
+
+
 def emit(row):
     print(json.dumps(row), flush=True)
 
@@ -70,8 +75,9 @@ def main():
     # oracle/wfpt_oracle.c; calibrated 0.87-1.01x against the reference's own
     # compiled kernels in the build container, profiles/r02/cpu_calibration.json),
     # 1 thread. The reference's compiled cdfdif exists only in the build
-    # container (oracle/_ref never travels), so the CDF row has a CPU number
-    # only there.
+    # container (oracle/_ref never travels); on the GPU box the CDF row's CPU
+    # baseline is the C restatement oracle/cdfdif_oracle.c (bit-exact to the
+    # reference's fixtures, tests/test_cdfdif.py).
     R = oracle
     C = oracle.load_ref_cdfdif()
     ctx = _lib.context(0)
@@ -200,9 +206,15 @@ def main():
         wall = timed(lambda: cdfdif_wrapper.dmat_cdf_array(xc, *p, 0.05, 0.1))
         s = xc[:5_000].copy()
         ref = cpu_rate(lambda: C.dmat_cdf_array(s, *p, 0.05, 0.1), s.size, cs) if C else None
+        # the C restatement of cdfdif (oracle/cdfdif_oracle.c, bit-exact to the
+        # reference's fixtures): 1 thread, and all host threads (OpenMP)
+        port1 = cpu_rate(lambda: R.dmat_cdf_array(s, *p, 0.05, 0.1), s.size, cs)
+        nt = threads()
+        portn = cpu_rate(lambda: R.dmat_cdf_array(xc, *p, 0.05, 0.1, n_threads=nt), xc.size, cs)
         emit({"row": f"(f)4 dmat_cdf_array {name} 100k", "trials": xc.size, "kernel_ms": k,
               "call_ms": wall * 1e3, "gpu_trials_per_s": xc.size / wall,
-              "cpu_ref_trials_per_s": ref})
+              "cpu_ref_trials_per_s": ref, "cpu_port_1thread_trials_per_s": port1,
+              "cpu_port_threads": nt, "cpu_port_all_threads_trials_per_s": portn})
 
 
 if __name__ == "__main__":

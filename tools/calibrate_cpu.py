@@ -7,7 +7,7 @@ on the same cores, the same inputs and the same loop shape (serial
 wiener_like), and records the ratio port/reference. Best of several
 interleaved rounds (the container is shared and noisy).
 
-    python tools/calibrate_cpu.py > profiles/r02/cpu_calibration.json
+    python tools/calibrate_cpu.py > profiles/r03/cpu_calibration.json
 """
 import json
 import os
@@ -56,8 +56,50 @@ def main():
             ref.append(rate(lambda: R.wiener_like(x, *args, *KN), n))
         assert oracle.wiener_like(x, *args, *KN) == R.wiener_like(x, *args, *KN)
         out["rows"].append({"dataset": name, "trials": n, "threads": 1,
+                            "loop": "serial wiener_like (wfpt.pyx:66-76)",
                             "port_trials_per_s": max(port), "reference_trials_per_s": max(ref),
                             "port_over_reference": max(port) / max(ref)})
+    # all host threads: the port's OpenMP pdf_array (what bench.py's
+    # cpu_baseline "value" runs) next to the reference's full_pdf under the
+    # prange of wfpt.pyx:40 compiled with -fopenmp (ref_shim.pdf_array_prange)
+    nt = len(os.sched_getaffinity(0))
+    out["threads_all"] = nt
+    for name, args, n in (("simple", SIMPLE, 2_000_000), ("full", FULL, 200_000)):
+        x = np.sign(rng.uniform(-0.27, 0.73, n)) * (0.3 + rng.gamma(2.0, 0.45, n))
+        kn = (KN[0], KN[1], KN[2], KN[3], KN[4])
+        port, ref = [], []
+        for _ in range(5):
+            port.append(rate(lambda: oracle.pdf_array(x, *args, kn[0], 0, kn[1], kn[2], kn[3],
+                                                      kn[4], 0, 0, n_threads=nt), n))
+            ref.append(rate(lambda: R.pdf_array_prange(x, *args, kn[0], kn[1], kn[2], kn[3],
+                                                       kn[4], nt), n))
+        a_ = oracle.pdf_array(x, *args, kn[0], 0, kn[1], kn[2], kn[3], kn[4], 0, 0, n_threads=nt)
+        b_ = R.pdf_array_prange(x, *args, kn[0], kn[1], kn[2], kn[3], kn[4], nt)
+        assert np.array_equal(a_, b_)
+        out["rows"].append({"dataset": name, "trials": n, "threads": nt,
+                            "loop": "pdf_array densities, OpenMP over trials (wfpt.pyx:40 "
+                                    "prange; -fopenmp is not the reference's own build)",
+                            "port_trials_per_s": max(port), "reference_trials_per_s": max(ref),
+                            "port_over_reference": max(port) / max(ref)})
+    # the DMAT CDF (cdfdif_wrapper.dmat_cdf_array): oracle/cdfdif_oracle.c vs
+    # the reference's own extension, 1 thread
+    C = oracle.load_ref_cdfdif()
+    if C is not None:
+        for name, args in (("cdf full", FULL), ("cdf simple", SIMPLE)):
+            n = 4000
+            x = np.sign(rng.uniform(-0.27, 0.73, n)) * (0.3 + rng.gamma(2.0, 0.45, n))
+            x = np.clip(x, -4.9, 4.9)
+            port, ref = [], []
+            for _ in range(5):
+                port.append(rate(lambda: oracle.dmat_cdf_array(x, *args, 0.05, 0.1), n))
+                ref.append(rate(lambda: C.dmat_cdf_array(x, *args, 0.05, 0.1), n))
+            assert np.array_equal(oracle.dmat_cdf_array(x, *args, 0.05, 0.1),
+                                  C.dmat_cdf_array(x, *args, 0.05, 0.1))
+            out["rows"].append({"dataset": name, "trials": n, "threads": 1,
+                                "loop": "dmat_cdf_array (cdfdif_wrapper.pyx:44-51)",
+                                "port_trials_per_s": max(port),
+                                "reference_trials_per_s": max(ref),
+                                "port_over_reference": max(port) / max(ref)})
     print(json.dumps(out, indent=1))
 
 
