@@ -980,6 +980,86 @@ __device__ inline void put5(double (&v)[5], int i, double x) {
 // (exp_val's range reduction would make NaN of it).
 __device__ inline double exp_sat(double x) { return exp(x); }
 
+// Small-time series and drift factor of a grid in one 2-D recurrence
+// (WFPT_SMALL_2D). Every term of pdf.pxi:55-57 times the drift factor of
+// pdf.pxi:95-101 is exp(phi(j, k)) with
+//   phi(j, k) = m (g_j + 2k)^2 + c_j,   j = 0..4 (z node), k = lower..upper,
+// a quadratic in (j, k) on the equally spaced grid: its second differences
+// are constants (8m in k, 2 m h^2 + d2 in j, 4 m h mixed), so the whole
+// 5 x K table follows from six exponentials by products (the 1-D form below
+// takes 2 per term k plus 3 for the drift). Values only, like the 1-D
+// recurrences: ~K^2/2 + K + 4 chained roundings (< 40 ulp at K <= 8), far
+// inside kTieBand. Returns false, and the caller evaluates the grid the 1-D
+// way, when a term or an intermediate ratio could leave the normal range
+// (every exponent is affine or quadratic over the table: its corners bound
+// it) or a node's series is not positive (the fix-up path's semantics).
+#ifndef WFPT_SMALL_2D
+#define WFPT_SMALL_2D 1
+#endif
+__device__ inline bool small_grid2d(const TNode& T, const ZGrid& G, double sv, double (&out)[5]) {
+  const int K = T.K;
+  if (K > 8) return false;
+  const int lower = (int)(-floor((K - 1) / 2.));
+  const int upper = (int)ceil((K - 1) / 2.);
+  const double m = T.m;
+  double c[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+    c[i] = (sv == 0) ? G.A[i] - (T.vvx * 0.5) : (G.A[i] - T.vvx) * T.cden;
+  const double lo2 = (double)(2 * lower);
+  const double u0 = G.g[0] + lo2, u4 = G.g[4] + (double)(2 * upper);
+  const double h = G.g[1] - G.g[0];
+  const double d1 = c[1] - c[0];
+  const double d2 = (c[2] - c[1]) - d1;
+  const double a00 = m * (u0 * u0) + c[0];  // phi(0, lower)
+  const double aR = m * (h * (2.0 * u0 + h)) + d1;  // phi(1, lower) - phi(0, lower)
+  const double aQj = (2.0 * m) * (h * h) + d2;
+  const double aP = (4.0 * m) * (u0 + 1.0);  // phi(0, lower + 1) - phi(0, lower)
+  const double aQk = 8.0 * m;
+  const double aQjk = (4.0 * m) * h;
+  const double cmax = fmax(fmax(fmax(c[0], c[1]), fmax(c[2], c[3])), c[4]);
+  const double cmin = fmin(fmin(fmin(c[0], c[1]), fmin(c[2], c[3])), c[4]);
+  const double U = fmax(fabs(u0), fabs(u4));
+  const double km1 = (double)(K - 1);
+  // j-ratios at the table's corners (j = 0..3, k = lower..upper), k-ratios at
+  // k = lower and upper - 1
+  const double rmax = fmax(fmax(fabs(aR), fabs(aR + 3.0 * aQj)),
+                           fmax(fabs(aR + km1 * aQjk), fabs((aR + 3.0 * aQj) + km1 * aQjk)));
+  const double pmax = fmax(fabs(aP), fabs(aP + (km1 - 1.0) * aQk));
+  const double qmax = fmax(fmax(fabs(aQj), fabs(aQk)), fabs(aQjk));
+  constexpr double B = 640.0;
+  const bool safe = (cmax < B) & (m * (U * U) + cmin > -B) & (fmax(fmax(rmax, pmax), qmax) < B);
+  if (!safe) return false;
+  double E0 = exp_val(a00), R0 = exp_val(aR), P = exp_val(aP);
+  const double Qj = exp_val(aQj), Qk = exp_val(aQk), Qjk = exp_val(aQjk);
+  double s[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) s[i] = 0.0;
+  double k2 = lo2;
+  for (int k = lower; k <= upper; ++k) {
+    double E = E0, R = R0;
+    s[0] = madd(G.g[0] + k2, E, s[0]);
+#pragma unroll
+    for (int i = 1; i < 5; ++i) {
+      E = E * R;
+      if (i < 4) R = R * Qj;
+      s[i] = madd(G.g[i] + k2, E, s[i]);
+    }
+    E0 = E0 * P;
+    P = P * Qk;
+    R0 = R0 * Qjk;
+    k2 = k2 + 2.0;
+  }
+  const double f = T.rn * T.sc;
+  bool clean = true;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    out[i] = s[i] * f;
+    clean = clean & (s[i] > 0) & !__builtin_isinf(out[i]);
+  }
+  return clean;
+}
+
 // pdf_sv at the 5 root-level z nodes of one t node (the values of
 // tnode_pdf_sv at each node to a few ulp):
 //   * small-t series: the exponents (g_j + 2k)^2 m are quadratic in j on the
@@ -1004,6 +1084,9 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     return true;
   }
   const int K = T.K;
+#if WFPT_SMALL_2D
+  if (T.small && small_grid2d(T, G, sv, out)) return true;
+#endif
   if (T.small) {
     const int lower = (int)(-floor((K - 1) / 2.));
     const int upper = (int)ceil((K - 1) / 2.);
@@ -1016,7 +1099,9 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
       // the lean pass), not held as arrays across the branch.
       const double w0 = G.g[0] + k2, w4 = G.g[4] + k2;
       const double e0 = (w0 * w0) * T.m, e4 = (w4 * w4) * T.m;
-      if (e0 > -600.0 && e4 > -600.0) {
+      // with WFPT_SMALL_2D the 2-D table above takes every grid it can, so
+      // this branch only sees the rare ones: node by node below
+      if (!WFPT_SMALL_2D && e0 > -600.0 && e4 > -600.0) {
         const double w1 = G.g[1] + k2, w2 = G.g[2] + k2;
         const double e1 = (w1 * w1) * T.m, e2 = (w2 * w2) * T.m;
         const double d1 = e1 - e0;
@@ -1306,18 +1391,23 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
 // exactly the bits the per-lane loop produces. The z grid is the call's table
 // (EngTables), shared by both.
 struct L0Hints {
-  double qn[5];
+  // q of t node j is q0 R^j (formed per node: two registers instead of five
+  // held across the node loop; the products are the ones a table would hold)
+  double q0, R;
   double ia2;  // 1 / a^2
   Decision D0, D4;
   bool ok0, ok4, shared;
   __device__ double qh(int j) const {
-    return j == 0 ? qn[0] : j == 1 ? qn[1] : j == 2 ? qn[2] : j == 3 ? qn[3] : qn[4];
+    if (q0 < 0.0) return -1.0;
+    const double R2 = R * R;
+    const double Rj = j == 1 ? R : j == 2 ? R2 : j == 3 ? R2 * R : R2 * R2;
+    return j == 0 ? q0 : q0 * Rj;
   }
 };
 __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, double err) {
   L0Hints H;
-#pragma unroll
-  for (int j = 0; j < 5; ++j) H.qn[j] = -1.0;
+  H.q0 = -1.0;
+  H.R = 0.0;
   H.D0 = Decision{0, 0, 0};
   H.D4 = Decision{0, 0, 0};
   H.ok0 = H.ok4 = H.shared = false;
@@ -1328,12 +1418,8 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
   const double q0 = exp((-kPi2 * ((x - lb) * ia2)) * 0.5);
   const double R = exp((kPi2 * (ub - lb)) * (0.125 * ia2));
   if (q0 > 1e-280 && R < 1e10 && x - lb > 0) {
-    const double R2 = R * R;
-    H.qn[0] = q0;
-    H.qn[1] = q0 * R;
-    H.qn[2] = q0 * R2;
-    H.qn[3] = q0 * (R2 * R);
-    H.qn[4] = q0 * (R2 * R2);
+    H.q0 = q0;
+    H.R = R;
   }
   if (x - ub > 0) {
     float args0, args4;
@@ -1375,7 +1461,10 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
 
 // The engine's level 0 of one trial (as fast_level0, on the table's z grid):
 // kFinal (p), kTree (f[], pend) or kExact.
-template <int MODE>
+// KEEP_F = false (the lean pass, which never reads f[]): the root Simpson
+// sums are accumulated as the t nodes complete, in the reference's
+// expression order (three registers across the node loop instead of five).
+template <int MODE, bool KEEP_F = true>
 __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs& K,
                                    const ZGrid& G, double& p, double (&f)[5], long long& ne,
                                    unsigned& pend, const double* stab = nullptr) {
@@ -1384,6 +1473,8 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
   if (!tr.valid) return kFinal;
   double lb, ub;
   tree_root<MODE>(tr, P, lb, ub);
+  // formed here: a one-bit mask across the node loop instead of a double
+  const bool structural = (MODE == kAdaptZ) ? tr.x - P.t <= 0 : tr.x - lb <= 0;
   int flags = 0;
   if (MODE == kAdaptZ) {
     const double iw = 1.0 / (ub - lb);
@@ -1395,6 +1486,36 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
     ne += 5;
   } else {
     const L0Hints H = l0_hints(tr.x, lb, ub, P.a, K.err);
+    if (!KEEP_F) {
+      // X, Y, Z after node j:  0: f0 | 1: f0, f0+4f1 | 2: f2, f0+4f2, Sl |
+      // 3: f2+4f3, f0+4f2, Sl | 4: -> S = h6((f0+4f2)+f4), Sr = h12((f2+4f3)+f4)
+      const double h = ub - lb;
+      double X = 0.0, Y = 0.0, Z = 0.0, y4 = 0.0;
+#pragma unroll 1
+      for (int j = 0; j < 5; ++j) {
+        bool pj;
+        const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);
+        if (flags & kFlagExact) return kExact;
+        if (pj) pend |= 1u << (j * (kTreeW / 4));
+        const double x4 = X + (4 * y);
+        if (j == 2) Z = (h / 12) * (Y + y);
+        Y = (j == 1 || j == 2) ? x4 : Y;
+        X = (j == 0 || j == 2) ? y : (j == 3 ? x4 : X);
+        y4 = y;
+      }
+      if (pend) return kTree;
+      Simp s;
+      s.S = (h / 6) * (Y + y4);
+      s.Sl = Z;
+      s.Sr = (h / 12) * (X + y4);
+      s.S2 = s.Sl + s.Sr;
+      const int bottom = K.n_st;
+      const bool refine = simpson_refine(s.S, s.S2, K.simps_err, bottom, flags);
+      if (flags & kFlagExact) return kExact;
+      if (refine) return kTree;
+      p = s.S2 + (s.S2 - s.S) / 15;
+      return (p > kExactBelow || structural) ? kFinal : kExact;
+    }
 #pragma unroll 1
     for (int j = 0; j < 5; ++j) {
       bool pj;
@@ -1415,7 +1536,6 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
   if (flags & kFlagExact) return kExact;
   if (refine) return kTree;
   p = s.S2 + (s.S2 - s.S) / 15;
-  const bool structural = (MODE == kAdaptZ) ? tr.x - P.t <= 0 : tr.x - lb <= 0;
   return (p > kExactBelow || structural) ? kFinal : kExact;
 }
 template <int MODE>

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "noasm": ["WFPT_HORNER_ASM=0"],
+    "s1d": ["WFPT_SMALL_2D=0"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 

@@ -37,7 +37,18 @@ def main():
                          "is 1e-4, hddm/likelihoods.py:30)")
     ap.add_argument("--seed", type=int, default=20261017)
     ap.add_argument("--sv", type=float, default=0.1, help="true sv with --full")
+    ap.add_argument("--p-outlier", type=float, default=0.05,
+                    help="the model's fixed p_outlier (HDDM's recommended 0.05; the data "
+                         "carry no outliers, so 0 is the correctly specified model)")
+    ap.add_argument("--slow-dump", default=None,
+                    help="save the data and the parameter table of the slowest batched "
+                         "likelihood call (npz) here")
+    ap.add_argument("--watchdog", type=float, default=0.0,
+                    help="dump every thread's stack and exit after this many seconds")
     a = ap.parse_args()
+    if a.watchdog > 0:
+        import faulthandler
+        faulthandler.dump_traceback_later(a.watchdog, exit=True)
     from hddm_amd.hierarchical import HDDM, gen_data
     t0 = time.perf_counter()
     sv = sz = st = 0.0
@@ -46,8 +57,27 @@ def main():
     data, truth = gen_data(n_subj=a.subjects, n_trials=a.trials, sv=sv, sz=sz, st=st,
                            seed=a.seed, dt=a.dt)
     t_gen = time.perf_counter() - t0
+    if a.progress:
+        print(f"data: {len(data)} trials in {t_gen:.1f}s", flush=True)
     m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st") if a.full else (),
-             seed=1)
+             p_outlier=a.p_outlier, seed=1)
+    if a.slow_dump:
+        ds, inner, worst = m.dataset, m.dataset.wiener_like_nodes, [0.0]
+
+        def timed(params, **kw):
+            t = time.perf_counter()
+            r = inner(params, **kw)
+            el = time.perf_counter() - t
+            if el > worst[0]:
+                worst[0] = el
+                np.savez(a.slow_dump, params=np.asarray(params), rt=data["rt"].to_numpy(),
+                         response=data["response"].to_numpy(),
+                         subj_idx=data["subj_idx"].to_numpy(),
+                         cond=(data["cond"] == "c1").to_numpy(), seconds=el)
+                if el > 1e-3:
+                    print(f"slowest call so far: {el * 1e3:.2f} ms", flush=True)
+            return r
+        ds.wiener_like_nodes = timed
     m.sample(a.burn, progress=a.progress or None)  # burn-in (untimed)
     c0, s0 = m.likelihood_calls, m.likelihood_seconds
     m.call_stats = {}
@@ -63,7 +93,8 @@ def main():
         "value": a.iters / el, "unit": "sweeps/s",
         "config": {"subjects": a.subjects, "trials_per_subject": a.trials,
                    "nodes": m.n_nodes, "trials": m.n_trials, "full_ddm": a.full,
-                   "iters": a.iters, "data_dt": a.dt, "seed": a.seed},
+                   "iters": a.iters, "data_dt": a.dt, "seed": a.seed,
+                   "p_outlier": a.p_outlier},
         "seconds": el, "extrapolated_sample_2000_s": 2000 * el / a.iters,
         "batched_likelihood_calls_per_sweep": calls / a.iters,
         "likelihood_fraction_of_time": lik_s / el,

@@ -1,0 +1,10 @@
+# rocprofv3 host-trap PC sampling of the headline bench (instruction-level
+# time attribution of the lean kernel). Separate from PMC passes.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+OUT=gpurun_out/pcs
+rm -rf $OUT; mkdir -p $OUT
+timeout -k 10 180 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval ${PCS_INTERVAL:-1} --output-format csv -d $OUT -o pcs -- python3 bench.py --steps ${STEPS:-30} --warmup 2 --no-cpu-baseline > $OUT/pcs.log 2>&1 || { echo "PCS_FAIL rc=$?"; tail -20 $OUT/pcs.log; exit 1; }
+ls -la $OUT
+echo pcs-done
