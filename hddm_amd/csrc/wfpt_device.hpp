@@ -929,6 +929,10 @@ __device__ inline double exp_val(double x) {
 // the host per call (RootGrids) so the lean pass reads them instead of
 // recomputing them per lane; bit-identical to the per-lane recurrence.
 constexpr int kSinK = 8;
+// WFPT_SIN_PREFETCH=0: each row of the table is loaded where it is used
+#ifndef WFPT_SIN_PREFETCH
+#define WFPT_SIN_PREFETCH 0
+#endif
 __host__ __device__ inline void sin_rot(const ZGrid& G, double (&sj)[5], double (&cj)[5]) {
   sj[0] = G.s0;
   cj[0] = G.c0;
@@ -1084,6 +1088,18 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     return true;
   }
   const int K = T.K;
+#if defined(WFPT_KO_SMALL) || defined(WFPT_KO_LARGE)
+  // timing experiments only (tools/ab_variants.py): wrong values
+#ifdef WFPT_KO_SMALL
+  if (T.small) {
+#else
+  if (!T.small) {
+#endif
+#pragma unroll
+    for (int i = 0; i < 5; ++i) out[i] = T.sc * 0.25;
+    return true;
+  }
+#endif
 #if WFPT_SMALL_2D
   if (T.small && small_grid2d(T, G, sv, out)) return true;
 #endif
@@ -1135,6 +1151,33 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     // values the recurrence below produces (sin_table), read with scalar
     // loads instead of carried in 15 vector registers per lane
     double e = T.m, r = T.m * T.q2;
+#if WFPT_SIN_PREFETCH
+    if (K <= kSinK) {
+      // each row's scalar loads are issued one row ahead of their use, so
+      // the wait overlaps the previous row's products
+      double row[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) row[i] = stab[5 + i];
+      for (int k = 1; k <= K; ++k) {
+        const int kq = k + 1 <= kSinK ? k + 1 : kSinK;
+        double nxt[5];
+#pragma unroll
+        for (int i = 0; i < 5; ++i) nxt[i] = stab[5 * kq + i];
+        if (k == 1) {
+#pragma unroll
+          for (int i = 0; i < 5; ++i) p[i] = T.m * row[i];
+        } else {
+          e = e * r;
+          r = r * T.q2;
+          const double ke = (double)k * e;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) p[i] = madd(ke, row[i], p[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) row[i] = nxt[i];
+      }
+    } else {
+#else
     if (K >= 1) {
 #pragma unroll
       for (int i = 0; i < 5; ++i) p[i] = T.m * stab[5 + i];
@@ -1148,6 +1191,7 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
         for (int i = 0; i < 5; ++i) p[i] = madd(ke, stab[5 * k + i], p[i]);
       }
     } else {
+#endif
       // beyond the table (err far below 1e-10): the recurrence one node at
       // a time (few live registers)
 #pragma unroll 1
@@ -1214,6 +1258,13 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 #pragma unroll
     for (int i = 0; i < 5; ++i) p[i] = p[i] * kPi;
   }
+#ifdef WFPT_KO_LDRIFT
+  if (!T.small) {  // timing experiment only: no drift factor
+#pragma unroll
+    for (int i = 0; i < 5; ++i) out[i] = p[i] * T.sc;
+    return true;
+  }
+#endif
   // exponent of the drift factor at each node (quadratic in g), formed where
   // it is used
   auto cexp = [&](int i) -> double {
@@ -1451,6 +1502,12 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
     flags |= kFlagExact;
     return 0.0;
   }
+#ifdef WFPT_KO_NODE
+  if (MODE == kAdaptTZ) {  // timing experiment only: no grid evaluation
+    ne += 5;
+    return T.sc * iw;
+  }
+#endif
   if (MODE == kAdaptTZ) {
     const double iZz = 1.0 / ((z + tr.sz / 2.) - (z - tr.sz / 2.));
     return inner_root(T, G, iZz, v, sv, a, K, flags, ne, pend, stab) * iw;

@@ -780,7 +780,12 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
+#if WFPT_LEAN_REVERSE
+  // blocks dispatched last take the first chunks (timing experiment)
+  const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kFastBlock + threadIdx.x;
+#else
   const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
+#endif
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
   if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
