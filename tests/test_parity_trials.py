@@ -366,3 +366,32 @@ def test_extreme_parameters_match_reference(gpu, oracle_lib, p):
             else:
                 terms = oracle_lib.pdf_array(x, *p, 1e-4, 1, 2, 2, 1, 1e-3, po, w)
                 assert abs(tot - math.fsum(terms)) <= 1e-11 * math.fsum(np.abs(terms)), (p, po)
+
+
+@pytest.mark.parametrize("case", ["tiny_tt", "many_terms", "big_drift", "sz_wide", "a_small"])
+def test_small_time_table_paths(gpu, oracle_lib, case):
+    """The small-time grid's 2-D recurrence (wfpt_device.hpp: small_grid2d)
+    and its node-by-node fallback: short decision times (8|m| beyond the
+    table's exponent bound: the fallback), small err (K up to 8 and past it),
+    large drift exponents (sv, v), wide z intervals and small a; per trial
+    |dlogp| < 1e-6 against the reference through pdf_array, and the resident
+    total (full sequence, then the predicted lean one) against its fsum."""
+    rng = np.random.default_rng(97)
+    n = 2048
+    args = {"tiny_tt": (0.8, 0.3, 1.5, 0.5, 0.2, 0.3, 0.05),
+            "many_terms": (0.5, 0.2, 2.0, 0.5, 0.1, 0.3, 0.1),
+            "big_drift": (3.5, 2.5, 2.5, 0.45, 0.1, 0.3, 0.1),
+            "sz_wide": (-1.0, 0.8, 1.8, 0.5, 0.9, 0.3, 0.1),
+            "a_small": (1.0, 0.5, 0.45, 0.5, 0.2, 0.2, 0.05)}[case]
+    err = 1e-12 if case == "many_terms" else 1e-4
+    t = args[5]
+    x = rng.choice([-1.0, 1.0], n) * (t + rng.gamma(1.5, 0.08 if case == "tiny_tt" else 0.35, n))
+    x[:4] = [t + 1e-4, -(t + 1e-3), t + 0.01, -(t + 0.02)]
+    ref = oracle_lib.pdf_array(x, *args, err, 1, 2, 2, 1, 1e-3, 0.05, 0.1)
+    got = gpu.pdf_array(x, *args, err, 1, 2, 2, 1, 1e-3, 0.05, 0.1)
+    assert_logp_parity(got, ref, case)
+    ds = gpu.Dataset(x)
+    want = math.fsum(ref)
+    for _ in range(2):  # full sequence, then the predicted one
+        tot = ds.wiener_like(*args, err, 2, 2, 1, 1e-3, 0.05, 0.1)
+        assert abs(tot - want) <= 1e-11 * math.fsum(np.abs(ref)), (case, tot, want)
