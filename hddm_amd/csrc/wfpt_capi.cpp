@@ -136,6 +136,8 @@ struct wfpt_ctx {
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
   DevBuf<unsigned char> redo;  // per chunk: the lean pass left it to the engine (0 at rest)
   int* tree_any = nullptr;   // device: some chunk refined in-wave (finalize reports + clears)
+  double* fin = nullptr;     // device: multi-block finalize scratch (3 x 64 doubles)
+  int* fin_ticket = nullptr; // device: its last-block ticket (0 at rest)
   int* prof = nullptr;       // device: 16 refinement work counters (PROF_EVALS)
   unsigned long long* phase = nullptr;  // device: engine phase cycles (diagnostic builds)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
@@ -380,7 +382,8 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   HIP_TRY(hipGetLastError());
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? 1 : 0,
                         c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
-                        eng ? d->hcount + d->parity : nullptr, c->tree_any, mirror);
+                        eng ? d->hcount + d->parity : nullptr, c->tree_any, mirror, c->fin,
+                        c->fin_ticket);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -580,6 +583,9 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->fin_ticket, sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->fin_ticket, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->prof, 16 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->prof, 0, 16 * sizeof(int));
   if (e == hipSuccess)
@@ -618,6 +624,8 @@ void wfpt_close(wfpt_ctx* c) {
   c->nd_par.release();
   if (c->n_defer) (void)hipFree(c->n_defer);
   if (c->tree_any) (void)hipFree(c->tree_any);
+  if (c->fin) (void)hipFree(c->fin);
+  if (c->fin_ticket) (void)hipFree(c->fin_ticket);
   c->redo.release();
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
@@ -944,7 +952,7 @@ int run_multi(wfpt_ctx* c, const double* dx, int64_t n, const double* const arra
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, 0, c->status, c->mres_dev, ++c->seq,
-                        c->stream);
+                        c->stream, nullptr, nullptr, nullptr, nullptr, c->fin, c->fin_ticket);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
   if (int rc = check_status_value(c->mres[2])) return rc;

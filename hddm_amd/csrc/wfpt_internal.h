@@ -96,7 +96,10 @@ constexpr int kResDeferred = 1, kResTree = 2;
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
                      const int* split_rd = nullptr, int* split_rs = nullptr,
-                     int* tree_any = nullptr, double* mirror = nullptr);
+                     int* tree_any = nullptr, double* mirror = nullptr,
+                     double* fin = nullptr, int* ticket = nullptr);
+// fin (device, 3 * 64 doubles) + ticket (device int, 0 at rest): scratch of the
+// multi-block finalize for large nb (nullptr: one block)
 // res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then
 // out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);

@@ -1015,27 +1015,44 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
 // pinned host memory. Resets the device status word. Fixed summation order
 // for a given nb: thread k owns partials k + 1024 j, loaded kFinLoads at a
 // time (all in flight together) and summed in j order; then a fixed tree.
+// Large nb (C2's 10M trials: 156k partials): one block is bound by a single
+// CU's load bandwidth (29 us), so gridDim.x = G > 1 blocks each reduce a
+// contiguous range the same way into fin[g] (sum), fin[kFinMaxBlocks + g]
+// (zero count), fin[2 kFinMaxBlocks + g] (defer bits), and the last block to
+// finish (agent-scope ticket) adds the G block results in g order. Fixed
+// order for a given (nb, G); G = 1 is the single-block order.
 constexpr int kFinLoads = 16;
+constexpr int kFinMaxBlocks = 64;
+constexpr int64_t kFinPerBlock = 8192;  // partials per block when split
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
                                                         int64_t nb, int defer_bits,
                                                         int* status, double* out,
                                                         unsigned long long seq,
                                                         const int* split_rd, int* split_rs,
-                                                        int* tree_any, double* mirror) {
+                                                        int* tree_any, double* mirror,
+                                                        double* fin, int* ticket) {
   __shared__ double ss[16];
   __shared__ long long sz[16];
   __shared__ int sd[16];
+  __shared__ int last;
+  const int G = gridDim.x;
+  int64_t lo = 0, hi = nb;
+  if (G > 1) {
+    const int64_t L = (nb + G - 1) / G;
+    lo = (int64_t)blockIdx.x * L;
+    hi = lo + L < nb ? lo + L : nb;
+  }
   double s = 0.0;
   long long z = 0;
   int def = 0;
-  for (int64_t b0 = threadIdx.x; b0 < nb; b0 += kFinLoads * 1024) {
+  for (int64_t b0 = lo + threadIdx.x; b0 < hi; b0 += kFinLoads * 1024) {
     double v[kFinLoads];
     int w[kFinLoads];
 #pragma unroll
     for (int j = 0; j < kFinLoads; ++j) {
       const int64_t b = b0 + (int64_t)j * 1024;
-      v[j] = b < nb ? part[b] : 0.0;
-      w[j] = b < nb ? zeros[b] : 0;
+      v[j] = b < hi ? part[b] : 0.0;
+      w[j] = b < hi ? zeros[b] : 0;
     }
 #pragma unroll
     for (int j = 0; j < kFinLoads; ++j) {
@@ -1064,6 +1081,32 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
       zz += sz[k];
       dd |= sd[k];
     }
+    if (G > 1) {
+      fin[blockIdx.x] = t;
+      fin[kFinMaxBlocks + blockIdx.x] = (double)zz;
+      fin[2 * kFinMaxBlocks + blockIdx.x] = (double)dd;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int prev =
+          __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == G - 1;
+    } else {
+      last = 1;
+    }
+    if (G > 1 && last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      t = 0.0;
+      zz = 0;
+      dd = 0;
+      for (int g = 0; g < G; ++g) {
+        t += __hip_atomic_load(&fin[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        zz += (long long)__hip_atomic_load(&fin[kFinMaxBlocks + g], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        dd |= (int)__hip_atomic_load(&fin[2 * kFinMaxBlocks + g], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *ticket = 0;  // ready for the next call (stream order)
+    }
+    if (!last) return;
     const int st = *status;
     *status = 0;
     out[0] = t;
@@ -1545,9 +1588,14 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
-                     const int* split_rd, int* split_rs, int* tree_any, double* mirror) {
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, s, part, zeros, nb, defer_bits,
-                     status, out, seq, split_rd, split_rs, tree_any, mirror);
+                     const int* split_rd, int* split_rs, int* tree_any, double* mirror,
+                     double* fin, int* ticket) {
+  int64_t g = 1;
+  if (fin && ticket && nb > 2 * kFinPerBlock)
+    g = std::min<int64_t>(kFinMaxBlocks, (nb + kFinPerBlock - 1) / kFinPerBlock);
+  hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)g), dim3(1024), 0, s, part, zeros, nb,
+                     defer_bits, status, out, seq, split_rd, split_rs, tree_any, mirror, fin,
+                     ticket);
 }
 
 template <int MODE, bool COUNT>
