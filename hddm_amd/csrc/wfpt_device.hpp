@@ -74,6 +74,20 @@ __host__ __device__ inline int select_mode(double sz, double st, int use_adaptiv
 // path's node values carry ~1e-14 relative error; the band is 1000x wider).
 constexpr double kExactBelow = 1e-290;
 constexpr double kTieBand = 1e-11;
+
+// UNROLL: the t-node loop fully unrolled (node positions, q hints and
+// accumulators without per-node selects or loop-carried copies; 5x the code).
+// The lean pass unrolls its boundary-uniform call site (WFPT_LEAN_UNROLL):
+// 127 VGPRs = 4 waves/SIMD instead of 168 = 3, and C3's level 0 -13%.
+#ifndef WFPT_LEAN_UNROLL
+#define WFPT_LEAN_UNROLL 1
+#endif
+// WFPT_FAST_L0_UNROLL: the same for the per-node and per-trial-parameter
+// level-0 passes (fast_level0: no scratch, node kernel -18%); the engine's
+// level 0 keeps the loop (measured: the unrolled copy slows its stress set 4%)
+#ifndef WFPT_FAST_L0_UNROLL
+#define WFPT_FAST_L0_UNROLL 1
+#endif
 enum Flag : int {
   kFlagDepth = 1,     // refinement deeper than the stack (WFPT_MAX_DEPTH)
   kFlagBudget = 2,    // more than kEvalBudget pdf_sv evaluations in one trial
@@ -1407,7 +1421,7 @@ __device__ inline void tree_root(const Trial& tr, const Params& P, double& lb, d
 //           node's z integral needs refinement (bit k of `pend`: tree point
 //           k * kTreeW / 4); f[] = the root interval's values at lb, d, c, e, ub;
 //   kExact: the value hinges on last-bit rounding (recomputed exactly).
-template <int MODE>
+template <int MODE, bool UNROLL = false>
 __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
                                  double& p, double (&f)[5], long long& ne, unsigned& pend);
 
@@ -1433,7 +1447,7 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
     G = zgrid_setup(z - tr.sz / 2., z + tr.sz / 2., v, sv, a);
   (void)t;
   (void)x;
-  return eng_level0<MODE>(x0, P, K, G, p, f, ne, pend);
+  return eng_level0<MODE, WFPT_FAST_L0_UNROLL != 0>(x0, P, K, G, p, f, ne, pend);
 }
 
 // The engine's level 0 (kAdaptT / kAdaptTZ): the same operations as
@@ -1521,7 +1535,7 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
 // KEEP_F = false (the lean pass, which never reads f[]): the root Simpson
 // sums are accumulated as the t nodes complete, in the reference's
 // expression order (three registers across the node loop instead of five).
-template <int MODE, bool KEEP_F = true>
+template <int MODE, bool KEEP_F = true, bool UNROLL = false>
 __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs& K,
                                    const ZGrid& G, double& p, double (&f)[5], long long& ne,
                                    unsigned& pend, const double* stab = nullptr) {
@@ -1548,18 +1562,26 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
       // 3: f2+4f3, f0+4f2, Sl | 4: -> S = h6((f0+4f2)+f4), Sr = h12((f2+4f3)+f4)
       const double h = ub - lb;
       double X = 0.0, Y = 0.0, Z = 0.0, y4 = 0.0;
+#define WFPT_L0_ACC_NODE(j)                                                      \
+  {                                                                              \
+    bool pj;                                                                     \
+    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab); \
+    if (flags & kFlagExact) return kExact;                                       \
+    if (pj) pend |= 1u << ((j) * (kTreeW / 4));                                  \
+    const double x4 = X + (4 * y);                                               \
+    if ((j) == 2) Z = (h / 12) * (Y + y);                                        \
+    Y = ((j) == 1 || (j) == 2) ? x4 : Y;                                         \
+    X = ((j) == 0 || (j) == 2) ? y : ((j) == 3 ? x4 : X);                        \
+    y4 = y;                                                                      \
+  }
+      if constexpr (UNROLL) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) WFPT_L0_ACC_NODE(j)
+      } else {
 #pragma unroll 1
-      for (int j = 0; j < 5; ++j) {
-        bool pj;
-        const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);
-        if (flags & kFlagExact) return kExact;
-        if (pj) pend |= 1u << (j * (kTreeW / 4));
-        const double x4 = X + (4 * y);
-        if (j == 2) Z = (h / 12) * (Y + y);
-        Y = (j == 1 || j == 2) ? x4 : Y;
-        X = (j == 0 || j == 2) ? y : (j == 3 ? x4 : X);
-        y4 = y;
+        for (int j = 0; j < 5; ++j) WFPT_L0_ACC_NODE(j)
       }
+#undef WFPT_L0_ACC_NODE
       if (pend) return kTree;
       Simp s;
       s.S = (h / 6) * (Y + y4);
@@ -1573,18 +1595,26 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
       p = s.S2 + (s.S2 - s.S) / 15;
       return (p > kExactBelow || structural) ? kFinal : kExact;
     }
+#define WFPT_L0_F_NODE(j)                                                        \
+  {                                                                              \
+    bool pj;                                                                     \
+    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab); \
+    if (flags & kFlagExact) return kExact;                                       \
+    if (pj) pend |= 1u << ((j) * (kTreeW / 4));                                  \
+    if ((j) == 0) f[0] = y;                                                      \
+    else if ((j) == 1) f[1] = y;                                                 \
+    else if ((j) == 2) f[2] = y;                                                 \
+    else if ((j) == 3) f[3] = y;                                                 \
+    else f[4] = y;                                                               \
+  }
+    if constexpr (UNROLL) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) WFPT_L0_F_NODE(j)
+    } else {
 #pragma unroll 1
-    for (int j = 0; j < 5; ++j) {
-      bool pj;
-      const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);
-      if (flags & kFlagExact) return kExact;
-      if (pj) pend |= 1u << (j * (kTreeW / 4));
-      if (j == 0) f[0] = y;
-      else if (j == 1) f[1] = y;
-      else if (j == 2) f[2] = y;
-      else if (j == 3) f[3] = y;
-      else f[4] = y;
+      for (int j = 0; j < 5; ++j) WFPT_L0_F_NODE(j)
     }
+#undef WFPT_L0_F_NODE
   }
   if (pend) return kTree;
   const Simp s = simp5(ub - lb, f[0], f[1], f[2], f[3], f[4]);
@@ -1595,10 +1625,10 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
   p = s.S2 + (s.S2 - s.S) / 15;
   return (p > kExactBelow || structural) ? kFinal : kExact;
 }
-template <int MODE>
+template <int MODE, bool UNROLL>
 __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
                                  double& p, double (&f)[5], long long& ne, unsigned& pend) {
-  return eng_level0_t<MODE>(trial_setup(x0, P), P, K, G, p, f, ne, pend);
+  return eng_level0_t<MODE, true, UNROLL>(trial_setup(x0, P), P, K, G, p, f, ne, pend);
 }
 
 // z grids of the engine, relative to the dyadic points P of [lb_z, ub_z]:

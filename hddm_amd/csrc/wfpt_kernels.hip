@@ -805,12 +805,12 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
   const int b = (bp == bo) ? 1 : 0;  // every trial upper: 1; otherwise lower first
   if (own && pos == (b != 0))
-    oc = eng_level0_t<MODE, false>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
+    oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
                                    zgrid_uniform(R, b), p, f0, ne0, pend0,
                                    WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
   if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
     if (own && pos)
-      oc = eng_level0_t<MODE, false>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
+      oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
                                      ne0, pend0, WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
   }
   if (__ballot(oc == kTree) != 0ull) {
