@@ -74,7 +74,7 @@ def host_threads():
 def cpu_baseline(x, budget_s):
     """The reference CPU path restated in C (oracle/wfpt_oracle.c, kind "port";
     calibrated against the reference's own kernels in the build container:
-    profiles/r02/cpu_calibration.json), timed on this host's cores:
+    profiles/r03/cpu_calibration.json), timed on this host's cores:
     1 thread = the reference's serial wiener_like loop (wfpt.pyx:66-76);
     all cores = the same per-trial full_pdf under OpenMP (the reference's
     prange in pdf_array, wfpt.pyx:40, built with -fopenmp)."""
@@ -104,7 +104,8 @@ def cpu_baseline(x, budget_s):
     return {"value": vn, "unit": "trials/s", "cores": nt, "kind": "port",
             "value_1_thread": v1,
             "sample": f"C restatement of wfpt.wiener_like (oracle/wfpt_oracle.c; port/reference "
-                      f"speed 1.01 measured in the build container): all {nt} host threads over "
+                      f"speed 1.03 on 1 thread, 1.26 on 8 OpenMP threads, measured in the build "
+                      f"container, BASELINE.md 3a): all {nt} host threads over "
                       f"the {allc.size} benchmark trials x{done // allc.size} ({eln:.1f} s); "
                       f"1 thread over the first {one.size} trials ({el1:.1f} s, "
                       f"{v1:.3e} trials/s)"}
