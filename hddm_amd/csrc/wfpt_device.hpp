@@ -1020,10 +1020,12 @@ __device__ inline bool small_grid2d(const TNode& T, const ZGrid& G, double sv, d
   const int lower = (int)(-floor((K - 1) / 2.));
   const int upper = (int)ceil((K - 1) / 2.);
   const double m = T.m;
+  // the drift exponent (A_i - vvx / 2 for sv = 0, (A_i - vvx) cden otherwise)
+  // as one expression: the multiplier 1 is exact, so no per-node select
+  const double dv = (sv == 0) ? T.vvx * 0.5 : T.vvx, dm = (sv == 0) ? 1.0 : T.cden;
   double c[5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i)
-    c[i] = (sv == 0) ? G.A[i] - (T.vvx * 0.5) : (G.A[i] - T.vvx) * T.cden;
+  for (int i = 0; i < 5; ++i) c[i] = (G.A[i] - dv) * dm;
   const double lo2 = (double)(2 * lower);
   const double u0 = G.g[0] + lo2, u4 = G.g[4] + (double)(2 * upper);
   const double h = G.g[1] - G.g[0];
@@ -1280,10 +1282,10 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
   }
 #endif
   // exponent of the drift factor at each node (quadratic in g), formed where
-  // it is used
-  auto cexp = [&](int i) -> double {
-    return (sv == 0) ? G.A[i] - (T.vvx * 0.5) : (G.A[i] - T.vvx) * T.cden;
-  };
+  // it is used: A_i - vvx / 2 for sv = 0, (A_i - vvx) cden otherwise, as one
+  // expression (the multiplier 1 is exact: no per-node select)
+  const double dv = (sv == 0) ? T.vvx * 0.5 : T.vvx, dm = (sv == 0) ? 1.0 : T.cden;
+  auto cexp = [&](int i) -> double { return (G.A[i] - dv) * dm; };
   double ex[5];
   const double c0 = cexp(0), c2 = cexp(2), c4 = cexp(4);
   const bool moderate = fabs(c0) < 600.0 && fabs(c2) < 600.0 && fabs(c4) < 600.0;
@@ -1304,7 +1306,7 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
 #pragma unroll 1
     for (int i = 0; i < 5; ++i) {
       const double Ai = pick5(G.A, i);
-      put5(ex, i, exp_sat((sv == 0) ? Ai - (T.vvx * 0.5) : (Ai - T.vvx) * T.cden));
+      put5(ex, i, exp_sat((Ai - dv) * dm));
     }
   }
   // the common case: every series value positive and every product finite;
