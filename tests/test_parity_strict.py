@@ -181,6 +181,32 @@ def test_call_sequence_determinism(gpu):
     assert host == b1
 
 
+@pytest.mark.gpu
+def test_call_sequence_determinism_multiblock_finalize(gpu, oracle_lib):
+    """The same bitwise call-history independence when the finalize runs as
+    several blocks (> 16k chunk partials: 1.5M trials, 23.4k chunks): the
+    full, predicted (lean / fast-only) and mispredicted sequences and the
+    host-array path give identical totals, and the total equals the
+    reference's per-trial fsum to 1e-11 relative."""
+    np.random.seed(11)
+    x = gpu.gen_rts_from_cdf(*PINNED, samples=1_500_000, dt=1e-3)
+    ds = gpu.Dataset(x)
+    kn = KN
+    defer = STRESS[1]
+    a = [ds.wiener_like(*PINNED, *kn) for _ in range(3)]
+    b1 = ds.wiener_like(*defer, *kn)  # mispredicted after the lean calls
+    b2 = ds.wiener_like(*defer, *kn)
+    a.append(ds.wiener_like(*PINNED, *kn))
+    assert a[0] == a[1] == a[2] == a[3], a
+    assert b1 == b2, (b1, b2)
+    xs = x[np.lexsort((np.abs(x), x > 0))]
+    assert gpu.wiener_like(xs, *PINNED, *kn) == a[0]
+    terms = oracle_lib.pdf_array(x[:200_000], *PINNED, kn[0], 1, *kn[1:])
+    ref_head = math.fsum(terms)
+    got_head = gpu.Dataset(x[:200_000]).wiener_like(*PINNED, *kn)
+    assert abs(got_head - ref_head) <= 1e-11 * math.fsum(np.abs(terms))
+
+
 def _flip(x, v, z):
     return (abs(x), -v, 1 - z) if x > 0 else (abs(x), v, z)
 
