@@ -342,6 +342,15 @@ __host__ __device__ inline double msub(double a, double b, double c) {
 #endif
 }
 
+// Exponentials of the single-node path (tnode_ftt / tnode_pdf_sv; defined
+// after exp_val): values only, the fitted exp with its argument clamped to
+// [-1100, 1100] (exp_val would make NaN of +-inf; the clamp keeps 0 / inf and
+// NaN). WFPT_NODE_FAST_EXP=0: OCML's exp.
+#ifndef WFPT_NODE_FAST_EXP
+#define WFPT_NODE_FAST_EXP 1
+#endif
+__device__ inline double exp_node(double x);
+
 // f(t|0,1,w) from a prepared t node (pdf.pxi:49-65).
 __device__ inline double tnode_ftt(const TNode& T, double w) {
   double p = 0.0;
@@ -351,7 +360,7 @@ __device__ inline double tnode_ftt(const TNode& T, double w) {
     const int upper = (int)ceil((K - 1) / 2.);
     for (int k = lower; k <= upper; ++k) {
       const double wk = w + (double)(2 * k);
-      p = madd(wk, exp((wk * wk) * T.m), p);
+      p = madd(wk, exp_node((wk * wk) * T.m), p);
     }
     p = p * T.rn;
   } else {
@@ -379,13 +388,13 @@ __device__ inline double tnode_pdf_sv(const TNode& T, double w, double v, double
   if (!T.pos) return 0.0;
   const double p = tnode_ftt(T, w);
   if (sv == 0) {
-    const double ex = exp((((-v) * a) * w) - (T.vvx * 0.5));
+    const double ex = exp_node((((-v) * a) * w) - (T.vvx * 0.5));
     return (p * ex) * T.sc;
   }
   if (p < 0) return __builtin_nan("");  // log(p < 0) in the reference
   const double azsv = (a * w) * sv;
   const double c = (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) * T.cden;
-  const double ec = exp(c);
+  const double ec = exp_node(c);
   const double r = (p * ec) * T.sc;
   if (__builtin_isinf(ec))  // exp(c) overflow: the literal form
     return (exp(log(p) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) /
@@ -997,6 +1006,15 @@ __device__ inline void put5(double (&v)[5], int i, double x) {
 // overflow): libm's exp, which gives 0 for -inf like the reference
 // (exp_val's range reduction would make NaN of it).
 __device__ inline double exp_sat(double x) { return exp(x); }
+
+__device__ inline double exp_node(double x) {
+#if WFPT_FAST_EXP && WFPT_NODE_FAST_EXP
+  x = x < -1100.0 ? -1100.0 : (x > 1100.0 ? 1100.0 : x);
+  return exp_val(x);
+#else
+  return exp(x);
+#endif
+}
 
 // Small-time series and drift factor of a grid in one 2-D recurrence
 // (WFPT_SMALL_2D). Every term of pdf.pxi:55-57 times the drift factor of
