@@ -156,6 +156,7 @@ struct wfpt_ctx {
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
+  bool small = true;           // WFPT_SMALL=0: one-block calls keep the separate finalize
   // WFPT_LEAN_TREE: the largest fraction of refining chunks (last call) for
   // which the lean pass + engine redo of those chunks beats the engine over
   // every chunk
@@ -375,6 +376,17 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   // passes)
   const bool eng = d && d->hcount && engine_family(P, K) &&
                    !(part & (wfpt::kPassLean | wfpt::kPassRedo));
+  // one block of trials, level-0 pass only (direct family, or the lean pass):
+  // level 0 and finalize in one launch (WFPT_SMALL=0: two launches)
+  const bool level0_only = adaptive && (engine_family(P, K)
+                                            ? part == (wfpt::kPassFast | wfpt::kPassLean)
+                                            : part == wfpt::kPassFast);
+  if (c->small && level0_only && !prof && !c->count && !mirror &&
+      wfpt::launch_small(dx, n, P, K, c->part.p, c->zero.p, c->status, W, out, ++c->seq,
+                         c->tree_any, c->stream)) {
+    HIP_TRY(hipGetLastError());
+    return WFPT_OK;
+  }
   const wfpt::Split S = eng ? split_of(d) : wfpt::Split{};
   wfpt::launch_trials(0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p, c->zero.p,
                       c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
@@ -567,6 +579,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
+  if (const char* sm = std::getenv("WFPT_SMALL")) c->small = std::strcmp(sm, "0") != 0;
   if (const char* lt = std::getenv("WFPT_LEAN_TREE")) c->lean_tree_max = std::atof(lt);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);

@@ -98,6 +98,13 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer
                      const int* split_rd = nullptr, int* split_rs = nullptr,
                      int* tree_any = nullptr, double* mirror = nullptr,
                      double* fin = nullptr, int* ticket = nullptr);
+// One-block call (n <= 256, direct or adaptive family, level-0 pass + the
+// finalize in one launch: the same result bits and completion word as
+// launch_trials(kPassFast [| kPassLean]) + launch_finalize). false: not
+// eligible, nothing launched.
+bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                  int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
+                  int* tree_any, hipStream_t s);
 // fin (device, 3 * 64 doubles) + ticket (device int, 0 at rest): scratch of the
 // multi-block finalize for large nb (nullptr: one block)
 // res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then

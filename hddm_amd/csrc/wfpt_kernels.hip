@@ -1015,6 +1015,44 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
 // pinned host memory. Resets the device status word. Fixed summation order
 // for a given nb: thread k owns partials k + 1024 j, loaded kFinLoads at a
 // time (all in flight together) and summed in j order; then a fixed tree.
+// The result slot of a call (finalize's last step, one thread): {sum, zero
+// count, encoded errors, flags, -, heavy chunks, #tree} and then the
+// completion word; resets the device status word.
+__device__ inline void fin_write(double t, long long zz, int dd, int* status, double* out,
+                                 unsigned long long seq, const int* split_rd, int* split_rs,
+                                 int* tree_any, double* mirror) {
+  const int st = *status;
+  *status = 0;
+  out[0] = t;
+  out[1] = (double)zz;
+  out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+  int res3 = dd ? kResDeferred : 0;
+  double ntree = 0.0;
+  if (tree_any) {
+    if (*tree_any) res3 |= kResTree;
+    ntree = (double)*tree_any;
+    *tree_any = 0;
+  }
+  out[6] = ntree;
+  out[3] = (double)res3;
+  // heavy chunks recorded for the next call (Split)
+  out[5] = split_rd ? (double)*split_rd : 0.0;
+  if (split_rs) *split_rs = 0;
+  if (mirror) {  // device copy of the result (the RCCL exchange reads it)
+    mirror[0] = out[0];
+    mirror[1] = out[1];
+    mirror[2] = out[2];
+    mirror[3] = out[3];
+    mirror[5] = out[5];
+    mirror[6] = out[6];
+  }
+  __threadfence_system();
+  // completion word, written after the results are visible: the host may
+  // poll it instead of waiting on the stream
+  reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
+  __threadfence_system();
+}
+
 // Large nb (C2's 10M trials: 156k partials): one block is bound by a single
 // CU's load bandwidth (29 us), so gridDim.x = G > 1 blocks each reduce a
 // contiguous range the same way into fin[g] (sum), fin[kFinMaxBlocks + g]
@@ -1107,36 +1145,116 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, cons
       *ticket = 0;  // ready for the next call (stream order)
     }
     if (!last) return;
-    const int st = *status;
-    *status = 0;
-    out[0] = t;
-    out[1] = (double)zz;
-    out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
-    int res3 = dd ? kResDeferred : 0;
-    double ntree = 0.0;
-    if (tree_any) {
-      if (*tree_any) res3 |= kResTree;
-      ntree = (double)*tree_any;
-      *tree_any = 0;
+    fin_write(t, zz, dd, status, out, seq, split_rd, split_rs, tree_any, mirror);
+  }
+}
+
+// One-block calls (n <= kFastBlock trials: an HDDM node's 250, the drop-in's
+// per-node call): the level-0 pass of the direct family (fast_kernel's
+// operations) or of the adaptive families (lean_kernel's), then the finalize
+// of the block's <= 4 chunk partials in the same launch, with finalize_kernel's
+// exact operations on them (thread k holds partial k, one wave sum, then the
+// 16 wave sums added in order, the 15 empty ones as +0.0), so the result and
+// the completion word are bit for bit those of the two-launch sequence. The
+// chunk partials and zero words are written as usual (a deferred pass after a
+// misprediction reads them).
+struct FinArgs {
+  int* status;
+  double* out;
+  unsigned long long seq;
+  int* tree_any;
+  int defer_bits;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, RootGrids R,
+                                                           FinArgs F) {
+  __shared__ double fp[kFastBlock / 64];
+  __shared__ int fz[kFastBlock / 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = threadIdx.x, c = wv;
+  const bool has = c * 64 < A.n;  // wave-uniform
+  const bool own = i < A.n;
+  double part = 0.0;
+  int zw = 0;
+  bool tree = false;  // lean: the chunk is left to the redo pass (no partial)
+  if (has) {
+    double p = 0.0, f0[5];
+    long long ne0 = 0;
+    unsigned pend0 = 0u;
+    int oc = kFinal;
+    if constexpr (MODE == kDirect) {
+      int flags = 0;
+      if (own) oc = fast_level0<MODE>(A.x[i], A.P, A.K, p, f0, ne0, flags, pend0);
+      double lp = 0.0;
+      int zero = 0;
+      if (own && oc == kFinal) emit<OUT_SUM>(A, i, p, lp, zero);
+      const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
+      part = wave_sum(lp);
+      zw = __popcll(__ballot(zero != 0)) | (anyd ? kZeroDefer : 0);
+    } else {
+      const double x0 = own ? A.x[i] : 0.0;
+      const bool pos = x0 > 0;
+      const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
+      const int b = (bp == bo) ? 1 : 0;
+      if (own && pos == (b != 0))
+        oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(
+            trial_setup_b(x0, A.P, b != 0), A.P, A.K, zgrid_uniform(R, b), p, f0, ne0, pend0,
+            WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
+      if (bp != 0ull && bp != bo) {
+        if (own && pos)
+          oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(
+              trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0, ne0, pend0,
+              WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
+      }
+      if (__ballot(oc == kTree) != 0ull) {
+        if (lane == 0) W.redo[c] = 1;  // the host runs the redo pass (lean_kernel)
+        part = 0.0;                    // (discarded: the call is reported deferred)
+        zw = kZeroDefer;
+        tree = true;
+      } else {
+        double lp = 0.0;
+        int zero = 0;
+        const bool defer = oc == kExact;
+        if (own && !defer) emit<OUT_SUM>(A, i, p, lp, zero);
+        const bool anyd = defer_slots(W, c, lane, defer, kFlagExact);
+        part = wave_sum(lp);
+        zw = __popcll(__ballot(zero != 0)) | (anyd ? kZeroDefer : 0);
+      }
     }
-    out[6] = ntree;
-    out[3] = (double)res3;
-    // heavy chunks recorded for the next call (Split)
-    out[5] = split_rd ? (double)*split_rd : 0.0;
-    if (split_rs) *split_rs = 0;
-    if (mirror) {  // device copy of the result (the RCCL exchange reads it)
-      mirror[0] = out[0];
-      mirror[1] = out[1];
-      mirror[2] = out[2];
-      mirror[3] = out[3];
-      mirror[5] = out[5];
-      mirror[6] = out[6];
+    if (lane == 0) {
+      if (!tree) A.out[c] = part;
+      A.zeros[c] = zw;
+      fp[wv] = part;
+      fz[wv] = zw;
     }
-    __threadfence_system();
-    // completion word, written after the results are visible: the host may
-    // poll it instead of waiting on the stream
-    reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
-    __threadfence_system();
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  const int nb = (int)((A.n + 63) / 64);
+  double s = 0.0;
+  long long z = 0;
+  int def = 0;
+  if (lane < nb) {
+    s += fp[lane];
+    z += fz[lane] & (kZeroDefer - 1);
+    def |= fz[lane];
+  }
+  def = F.defer_bits ? (def & kZeroDefer) : 0;
+  s = wave_sum(s);
+  z = wave_sum_ll(z);
+  const bool anyd = __ballot(def != 0) != 0ull;
+  if (lane == 0) {
+    double t = 0.0;
+    long long zz = 0;
+    int dd = 0;
+    const double ss[2] = {s, 0.0};
+    for (int k = 0; k < 16; ++k) {
+      t += ss[k == 0 ? 0 : 1];
+      zz += k == 0 ? z : 0ll;
+      dd |= k == 0 ? (int)anyd : 0;
+    }
+    fin_write(t, zz, dd, F.status, F.out, F.seq, nullptr, nullptr, F.tree_any, nullptr);
   }
 }
 
@@ -1584,6 +1702,35 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
       launch_mode<false, OUT_ARRAY>(mode, part, A, W, S, s, fast_done);
     else launch_mode<false, OUT_LOGP>(mode, part, A, W, S, s, fast_done);
   }
+}
+
+bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                  int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
+                  int* tree_any, hipStream_t s) {
+  if (n <= 0 || n > kFastBlock) return false;
+  const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  if (mode > kAdaptTZ) return false;
+  const TrialArgs A = trial_args(x, n, P, K, part, zeros, nullptr, status, 0);
+  Work F = W;
+  F.redo = mode == kDirect ? nullptr : W.redo;
+  RootGrids R{};
+  if (mode != kDirect) root_grids(P, R);
+  const FinArgs Fa{status, out, seq, tree_any, 1};
+  switch (mode) {
+    case kDirect:
+      hipLaunchKernelGGL(small_kernel<kDirect>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
+      break;
+    case kAdaptT:
+      hipLaunchKernelGGL(small_kernel<kAdaptT>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
+      break;
+    case kAdaptZ:
+      hipLaunchKernelGGL(small_kernel<kAdaptZ>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
+      break;
+    default:
+      hipLaunchKernelGGL(small_kernel<kAdaptTZ>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
+      break;
+  }
+  return true;
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,

@@ -207,6 +207,33 @@ def test_call_sequence_determinism_multiblock_finalize(gpu, oracle_lib):
     assert abs(got_head - ref_head) <= 1e-11 * math.fsum(np.abs(terms))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 200, 250, 256])
+def test_one_block_calls_match_two_launch_sequence(gpu, oracle_lib, n):
+    """Datasets of <= 256 trials (an HDDM node) run level 0 and the finalize
+    in one launch once the call sequence is predicted (small_kernel): the
+    totals are bit for bit those of the first call's full two-launch
+    sequence, for the direct and the adaptive families, and after a
+    misprediction (a parameter set that defers, then one that does not)."""
+    rng = np.random.default_rng(n)
+    x = rng.choice([-1.0, 1.0], n) * (0.32 + rng.gamma(2.0, 0.4, n))
+    simple = (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0)
+    for args in (simple, PINNED, STRESS[3]):
+        ds = gpu.Dataset(x)
+        first = ds.wiener_like(*args, *KN)   # full sequence (two launches)
+        again = [ds.wiener_like(*args, *KN) for _ in range(3)]  # predicted: one launch
+        assert all(v == first for v in again), (n, args, first, again)
+        terms = oracle_lib.pdf_array(x, *args, KN[0], 1, *KN[1:])
+        ref = math.fsum(terms)
+        assert abs(first - ref) <= 1e-11 * math.fsum(np.abs(terms)) + 1e-300, (n, args)
+    ds = gpu.Dataset(x)
+    a0 = ds.wiener_like(*PINNED, *KN)
+    b = [ds.wiener_like(*STRESS[1], *KN) for _ in range(2)]  # mispredicted, then full
+    a1 = ds.wiener_like(*PINNED, *KN)
+    a2 = ds.wiener_like(*PINNED, *KN)
+    assert b[0] == b[1] and a0 == a1 == a2, (a0, a1, a2, b)
+
+
 def _flip(x, v, z):
     return (abs(x), -v, 1 - z) if x > 0 else (abs(x), v, z)
 
