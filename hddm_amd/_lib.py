@@ -108,6 +108,15 @@ try:  # diagnostics only: A/B runs may load an older library build without it
 except AttributeError:
     wfpt_profile_lists = wfpt_debug_waves = None
 wfpt_synchronize = _sig("wfpt_synchronize", _I, [_VP])
+wfpt_wiener_like_trials = _sig("wfpt_wiener_like_trials", _I, [_VP, _VP, _PP, _PK, _PD, _PD])
+wfpt_dataset_order = _sig("wfpt_dataset_order", _I, [_VP, ctypes.POINTER(_I64)])
+wfpt_debug_partials = _sig("wfpt_debug_partials", _I,
+                           [_VP, _PD, ctypes.POINTER(ctypes.c_int32), _I64])
+wfpt_last_path = _sig("wfpt_last_path", _I, [_VP, ctypes.POINTER(_I)])
+wfpt_wiener_like_local = _sig("wfpt_wiener_like_local", _I, [_VP, _VP, _PP, _PK, _PD])
+# WFPT_PATH_* (include/wfpt_amd.h): kernels the last likelihood call launched
+PATH_LEAN, PATH_ENGINE, PATH_SMALL, PATH_REDO = 1, 2, 4, 8
+PATH_FOLD, PATH_DIRECT, PATH_FIXED, PATH_SPLIT = 16, 32, 64, 128
 wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
 EXPORTED = [
@@ -120,6 +129,8 @@ EXPORTED = [
     "wfpt_wiener_like_multi_resident", "wfpt_comm_exchange_id", "wfpt_comm_init_tcp",
     "wfpt_comm_init_all", "wfpt_wiener_like_allreduce_group", "wfpt_result_poison",
     "wfpt_wiener_like_nodes_ex", "wfpt_wiener_like_multi_ex", "wfpt_wiener_like_multi_resident_ex",
+    "wfpt_wiener_like_trials", "wfpt_dataset_order", "wfpt_debug_partials", "wfpt_last_path",
+    "wfpt_wiener_like_local",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)
@@ -205,7 +216,8 @@ class Context:
             return {}
         check(wfpt_profile_lists(self.handle, a, 1 if reset else 0))
         v = list(a)
-        return {"tasks1": v[1], "tasks2": v[2], "records": v[4], "exact": v[5],
+        return {"segments": v[0], "node_deferred": v[3],
+                "tasks1": v[1], "tasks2": v[2], "records": v[4], "exact": v[5],
                 "walk": v[6], "zwalks": v[7], "zwalks0": v[8], "zwalks1": v[9],
                 "zwalks2": v[10], "phase_kcycles": v[11:16]}
 
@@ -217,6 +229,20 @@ class Context:
 
     def synchronize(self):
         check(wfpt_synchronize(self.handle))
+
+    def last_path(self):
+        """WFPT_PATH_* bits of the kernels the last likelihood call launched."""
+        v = _I()
+        check(wfpt_last_path(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def partials(self, n):
+        """The first n chunk partials {sum, zero word} of the last summing call."""
+        part = np.empty(n, dtype=np.float64)
+        zero = np.empty(n, dtype=np.int32)
+        check(wfpt_debug_partials(self.handle, dptr(part),
+                                  zero.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n))
+        return part, zero
 
 
 _ctx_lock = threading.Lock()

@@ -66,17 +66,20 @@ def build(force=False, verbose=False, defines=(), out=None):
             with open(lib + ".src", "w") as fh:
                 fh.write(source_digest(defines) + "\n")
         return lib
-    objs = []
+    objs, procs = [], []
     tag = os.path.splitext(os.path.basename(lib))[0]
-    for src in SOURCES:
+    for src in SOURCES:  # the translation units compile concurrently
         obj = os.path.join(LIBDIR, tag + "_" + os.path.splitext(src)[0] + ".o")
         flags = [f for d in defines if d.startswith("-") for f in d.split()]
         cmd = [HIPCC, *CFLAGS, *flags, *[f"-D{d}" for d in defines if not d.startswith("-")],
                "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     tmp = lib + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs,
            "-L/opt/rocm/lib", "-lrccl", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]

@@ -124,7 +124,10 @@ struct wfpt_ctx {
   DevBuf<double> x;       // uploads of host arrays
   DevBuf<double> part;    // block partial sums
   DevBuf<int> zero;       // block zero counts
-  DevBuf<double> res;     // final {sum, zeros} or per-node results
+  DevBuf<double> res;     // per-node results
+  double* ar = nullptr;   // device: this rank's {sum, zeros, errors, ...} of an all-reduce
+                          // call (8 doubles, allocated at open: a failed workspace reserve
+                          // cannot keep a rank out of the exchange)
   DevBuf<double> lp;      // per-trial outputs
   DevBuf<double> marr;    // wiener_like_multi parameter arrays
   DevBuf<double*> mptr;
@@ -143,6 +146,7 @@ struct wfpt_ctx {
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
+  DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
   int* n_defer = nullptr;    // device: deferred count of the per-node fast path (0 at rest)
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
@@ -166,6 +170,10 @@ struct wfpt_ctx {
   double k_ms = 0.0;
   int64_t launches = 0;
   int64_t n_evals = 0;
+  // per-trial check (wfpt_wiener_like_trials): device buffer of the call's
+  // per-trial log terms (the summing kernels' OUT_BOTH build), else null
+  double* trial = nullptr;
+  int path = 0;  // WFPT_PATH_* bits of the kernels the last likelihood call launched
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -203,8 +211,8 @@ struct wfpt_ds {
   int* hzn = nullptr;
   mutable int nsplit = 0;  // chunks the next call splits
   mutable int parity = 0;
-  // node datasets: the caller's index of each stored trial (per-trial
-  // outputs of wfpt_wiener_like_nodes_ex are returned in the caller's order)
+  // the caller's index of each stored trial (per-trial outputs are returned
+  // in the caller's order); empty = identity (WFPT_DS_INPUT_ORDER)
   std::vector<int64_t> perm;
 };
 
@@ -366,6 +374,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   wfpt::Work W;
   if (int rc = reserve_work(c, n, &W)) return rc;
   const bool adaptive = wfpt::has_deferred_pass(P, K);
+  if (part & wfpt::kPassFast) c->path = 0;  // a call sequence starts
   if (c->count && (part & wfpt::kPassFast))
     HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   // profiling: ev0..ev1 bracket the level-0 fast kernel (the dominant kernel,
@@ -381,16 +390,29 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   const bool level0_only = adaptive && (engine_family(P, K)
                                             ? part == (wfpt::kPassFast | wfpt::kPassLean)
                                             : part == wfpt::kPassFast);
+  const bool direct = adaptive && !engine_family(P, K);
   if (c->small && level0_only && !prof && !c->count && !mirror &&
       wfpt::launch_small(dx, n, P, K, c->part.p, c->zero.p, c->status, W, out, ++c->seq,
-                         c->tree_any, c->stream)) {
+                         c->tree_any, c->stream, c->trial)) {
     HIP_TRY(hipGetLastError());
+    c->path |= WFPT_PATH_SMALL | (direct ? WFPT_PATH_DIRECT : WFPT_PATH_LEAN);
     return WFPT_OK;
   }
   const wfpt::Split S = eng ? split_of(d) : wfpt::Split{};
-  wfpt::launch_trials(0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p, c->zero.p,
-                      c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
-                      prof ? c->ev1 : nullptr, &S);
+  wfpt::launch_trials(c->trial ? 3 : 0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p,
+                      c->zero.p, c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
+                      prof ? c->ev1 : nullptr, &S, c->trial);
+  if (!adaptive) {
+    c->path |= WFPT_PATH_FIXED;
+  } else {
+    if (part & wfpt::kPassFast)
+      c->path |= direct ? WFPT_PATH_DIRECT
+                        : (part & wfpt::kPassLean)
+                              ? WFPT_PATH_LEAN
+                              : (WFPT_PATH_ENGINE | (S.n > 0 ? WFPT_PATH_SPLIT : 0));
+    if (!direct && (part & wfpt::kPassRedo)) c->path |= WFPT_PATH_REDO;
+    if (part & wfpt::kPassDeferred) c->path |= WFPT_PATH_FOLD;
+  }
   HIP_TRY(hipGetLastError());
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? 1 : 0,
                         c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
@@ -530,6 +552,14 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
   return finish_sum(c, d, P, K, out, lean);
 }
 
+// |a| < |b| with NaN RTs last: a strict weak order for any input (the
+// dataset sorts must not hit std::stable_sort's undefined behaviour)
+bool abs_less_nan_last(double a, double b) {
+  const bool na = std::isnan(a), nb = std::isnan(b);
+  if (na || nb) return !na && nb;
+  return std::fabs(a) < std::fabs(b);
+}
+
 int upload(wfpt_ctx* c, const double* x, int64_t n) {
   HIP_TRY(c->x.reserve(std::max<int64_t>(n, 1)));
   if (n > 0)
@@ -597,6 +627,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->ar, 8 * sizeof(double));
+  if (e == hipSuccess) e = hipMemset(c->ar, 0, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin_ticket, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->fin_ticket, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->prof, 16 * sizeof(int));
@@ -635,10 +667,12 @@ void wfpt_close(wfpt_ctx* c) {
   c->defer.release();
   c->nd_idx.release();
   c->nd_par.release();
+  c->nd_chunks.release();
   if (c->n_defer) (void)hipFree(c->n_defer);
   if (c->tree_any) (void)hipFree(c->tree_any);
   if (c->fin) (void)hipFree(c->fin);
   if (c->fin_ticket) (void)hipFree(c->fin_ticket);
+  if (c->ar) (void)hipFree(c->ar);
   c->redo.release();
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
@@ -695,7 +729,7 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
     if (!keep_order)
       for (int32_t j = 0; j < n_nodes; ++j)
         std::stable_sort(idx.begin() + off[j], idx.begin() + off[j + 1],
-                         [&](int64_t a, int64_t b) { return std::fabs(rt[a]) < std::fabs(rt[b]); });
+                         [&](int64_t a, int64_t b) { return abs_less_nan_last(rt[a], rt[b]); });
   } else if (!keep_order) {
     // boundary first (x > 0 is the upper boundary, pdf.pxi:116), then |rt|:
     // the lean pass keeps a wave's root z grid in scalar registers when the
@@ -704,9 +738,7 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
     std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
       const bool ua = rt[a] > 0, ub = rt[b] > 0;
       if (ua != ub) return ub;
-      const bool na = std::isnan(rt[a]), nb = std::isnan(rt[b]);
-      if (na || nb) return !na && nb;
-      return std::fabs(rt[a]) < std::fabs(rt[b]);
+      return abs_less_nan_last(rt[a], rt[b]);
     });
   }
   std::vector<double> hx(n);
@@ -718,7 +750,7 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
   auto* d = new wfpt_ds();
   d->ctx = c;
   d->n = n;
-  if (node_id) d->perm = idx;
+  if (!keep_order || node_id) d->perm = idx;
   d->input_order = (flags & WFPT_DS_INPUT_ORDER) != 0;
   d->n_nodes = node_id ? n_nodes : 0;
   hipError_t e = hipMalloc((void**)&d->x, std::max<int64_t>(n, 1) * sizeof(double));
@@ -794,6 +826,67 @@ int wfpt_wiener_like(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p, const 
   if (rc >= 0) return rc;
   if (int rc2 = run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassAll, d)) return rc2;
   return finish_sum(c, d, P, K, out, false);
+}
+
+int wfpt_wiener_like_trials(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
+                            const wfpt_knobs* k, double* out, double* out_trial) {
+  if (!c || !d || !p || !k || !out || (!out_trial && d && d->n > 0))
+    return fail(WFPT_ERR_ARG, "null pointer");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (!p_outlier_in_range(P.p_outlier)) {  // wfpt.pyx:63-64: no trial is scored
+    *out = -INFINITY;
+    for (int64_t i = 0; i < d->n; ++i) out_trial[i] = -INFINITY;
+    return WFPT_OK;
+  }
+  WFPT_RANGE("wfpt_wiener_like_trials");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
+  c->trial = c->lp.p;
+  int rc = run_sum_fast(c, d, P, K, out);
+  if (rc < 0) {
+    rc = run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassAll, d);
+    if (rc == WFPT_OK) rc = finish_sum(c, d, P, K, out, false);
+  }
+  c->trial = nullptr;
+  if (rc != WFPT_OK) return rc;
+  if (d->n > 0) {
+    std::vector<double> h(d->n);
+    HIP_TRY(hipMemcpy(h.data(), c->lp.p, d->n * sizeof(double), hipMemcpyDeviceToHost));
+    if (d->perm.empty()) std::memcpy(out_trial, h.data(), d->n * sizeof(double));
+    else
+      for (int64_t i = 0; i < d->n; ++i) out_trial[d->perm[i]] = h[i];
+  }
+  return WFPT_OK;
+}
+
+int wfpt_dataset_order(const wfpt_ds* d, int64_t* perm) {
+  if (!d || (!perm && d->n > 0)) return fail(WFPT_ERR_ARG, "null pointer");
+  for (int64_t i = 0; i < d->n; ++i) perm[i] = d->perm.empty() ? i : d->perm[i];
+  return WFPT_OK;
+}
+
+int wfpt_debug_partials(wfpt_ctx* c, double* part, int32_t* zero, int64_t n) {
+  if (!c || n < 0 || (n > 0 && (!part || !zero))) return fail(WFPT_ERR_ARG, "bad arguments");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  if ((size_t)n > c->part.cap || (size_t)n > c->zero.cap)
+    return fail(WFPT_ERR_ARG, "more partials requested than the last calls wrote");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (n > 0) {
+    HIP_TRY(hipMemcpy(part, c->part.p, n * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(zero, c->zero.p, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  return WFPT_OK;
+}
+
+int wfpt_last_path(wfpt_ctx* c, int* path) {
+  if (!c || !path) return fail(WFPT_ERR_ARG, "null pointer");
+  std::lock_guard<std::mutex> lk(c->mu);
+  *path = c->path;
+  return WFPT_OK;
 }
 
 int wfpt_wiener_like_host(wfpt_ctx* c, const double* x, int64_t n, const wfpt_params* p,
@@ -874,9 +967,12 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   if (mode > wfpt::kAdaptTZ) mode = -1;  // fixed Simpson: generic kernel
   if (c->nodes_generic) mode = -1;
   HIP_TRY(c->res.reserve(std::max<int32_t>(m, 1)));
-  if (mode >= 0) {  // deferred-trial records of the per-node fast path
-    HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
-    HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
+  if (mode >= 0) {  // deferred records / listed chunks of the per-node fast path
+    if (mode == wfpt::kDirect) {
+      HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
+      HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
+    }
+    HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>((d->n + 63) / 64, 1)));
     HIP_TRY(hipMemsetAsync(c->n_defer, 0, sizeof(int), c->stream));
   }
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
@@ -884,8 +980,8 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, mode, c->lp.p, c->nd_idx.p,
-                     c->nd_par.p, c->n_defer, c->count ? c->evals : nullptr, c->status,
-                     c->stream);
+                     c->nd_par.p, c->n_defer, c->nd_chunks.p, c->count ? c->evals : nullptr,
+                     c->status, c->prof, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   ++c->seq;
@@ -1140,23 +1236,22 @@ namespace {
 // single process can overlap its devices (wfpt_wiener_like_allreduce_group):
 // ar_launch enqueues the level-0 pass (+ the deferred pass unless the lean
 // prediction applies) whose finalize leaves {sum, #zeros, errors} in the
-// device buffer c->res.p; ar_settle waits for a lean call's level-0 result
-// and, on a misprediction, enqueues the redo + fold passes and a second
-// finalize over the intact chunk partials (an unconditional redo launch would
-// dispatch one wave per chunk: ~48k blocks at 12.5M trials). After ar_settle,
-// c->res.p holds the rank's triple in stream order.
+// context's dedicated device triple c->ar; ar_settle waits for a lean call's
+// level-0 result and, on a misprediction, enqueues the redo + fold passes and
+// a second finalize over the intact chunk partials (an unconditional redo
+// launch would dispatch one wave per chunk: ~48k blocks at 12.5M trials).
+// After ar_settle, c->ar holds the rank's triple in stream order.
 struct ArState {
-  bool eng = false, lean = false;
+  bool eng = false, lean = false, launched = false;
 };
 int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               ArState* st) {
-  HIP_TRY(c->res.reserve(8));
   st->eng = engine_family(P, K);
   st->lean = st->eng && lean_predicted(c, d) && !c->count;
+  st->launched = true;
   if (st->lean)
-    return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d,
-                   c->res.p);
-  return run_sum(c, d->x, d->n, P, K, c->res.p, wfpt::kPassAll, d);
+    return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d, c->ar);
+  return run_sum(c, d->x, d->n, P, K, c->ar, wfpt::kPassAll, d);
 }
 int ar_settle(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               const ArState& st) {
@@ -1164,13 +1259,13 @@ int ar_settle(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::
   if (int rc = wait_result(c, c->mres)) return rc;
   if (res_deferred(c->mres))
     return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassDeferred | wfpt::kPassRedo, d,
-                   c->res.p);
+                   c->ar);
   return WFPT_OK;
 }
 // After the exchange: the summed triple to the mapped slot with a fresh
 // completion word (the local finalize used the previous one), then decode.
 int ar_finish(wfpt_ctx* c, const wfpt_ds* d, const ArState& st, double* out) {
-  wfpt::launch_publish(c->res.p, c->mres_dev, ++c->seq, c->stream);
+  wfpt::launch_publish(c->ar, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
   split_advance(d, st.eng && !st.lean, c->mres);
@@ -1178,27 +1273,47 @@ int ar_finish(wfpt_ctx* c, const wfpt_ds* d, const ArState& st, double* out) {
   if (rc == WFPT_OK && st.eng) note_tree(d, c->mres);
   return rc;
 }
+// A call that failed after its passes may have been enqueued: the dataset's
+// heavy-chunk record (written by an engine pass into the next parity's list)
+// and its predictions are reset, so the next call starts from a consistent
+// state (no split, the full call sequence).
+void ar_reset(wfpt_ctx* c, const wfpt_ds* d) {
+  if (!d) return;
+  (void)hipStreamSynchronize(c->stream);
+  d->nsplit = 0;
+  d->no_defer = false;
+  d->no_tree = false;
+  d->tree_frac = 1.0;
+  if (d->hcount) (void)hipMemset(d->hcount, 0, 2 * sizeof(int));
+}
 }  // namespace
 
 extern "C" {
 
 int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
                                const wfpt_knobs* k, double* out) {
-  if (!c || !d || !p || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (!c) return fail(WFPT_ERR_ARG, "null context");
+  // no communicator: no collective exists that a peer could be waiting in
   if (!c->comm) return fail(WFPT_ERR_ARG, "wfpt_comm_init was not called");
-  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
-  const wfpt::Params P = to_params(p);
-  const wfpt::Knobs K = to_knobs(k);
-  if (!p_outlier_in_range(P.p_outlier)) {  // uniform on every rank: no exchange needed
-    *out = -INFINITY;
+  // every exit below, once the communicator exists, goes through the exchange
+  if (p && !p_outlier_in_range(p->p_outlier) && d && k && out &&
+      d->ctx == c) {
+    *out = -INFINITY;  // the same parameters on every rank: no exchange needed
     return WFPT_OK;
   }
   WFPT_RANGE("wfpt_wiener_like_allreduce");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   ArState st;
-  int lrc = ar_launch(c, d, P, K, &st);
-  if (lrc == WFPT_OK) lrc = ar_settle(c, d, P, K, st);
+  int lrc = WFPT_OK;
+  if (!d || !p || !k || !out) lrc = fail(WFPT_ERR_ARG, "null pointer");
+  else if (d->ctx != c) lrc = fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  if (lrc == WFPT_OK) {
+    const wfpt::Params P = to_params(p);
+    const wfpt::Knobs K = to_knobs(k);
+    lrc = ar_launch(c, d, P, K, &st);
+    if (lrc == WFPT_OK) lrc = ar_settle(c, d, P, K, st);
+  }
   // fault injection for the failure path's tests (WFPT_FAULT=allreduce_local:
   // this rank's local pass reports a failure after it ran)
   if (lrc == WFPT_OK) {
@@ -1209,19 +1324,19 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   std::string lmsg;
   if (lrc != WFPT_OK) {
     // A rank that failed locally still enters the collective, with a
-    // poisoned triple (kPeerFailUnit), so that no peer waits on it forever;
-    // every peer then decodes "a rank failed" and this rank returns its own
-    // error. Only a broken stream (a sticky device fault) cannot enqueue the
-    // exchange: the communicator is then aborted.
+    // poisoned triple (kPeerFailUnit) written by a one-thread kernel into its
+    // preallocated device triple (nothing on the host stack is read after
+    // this call returns), so no peer waits on it forever; every peer then
+    // decodes "a rank failed" and this rank returns its own error. Only a
+    // broken stream (a sticky device fault) cannot enqueue the exchange: the
+    // communicator is then aborted.
     lmsg = g_last_error;
-    double poison[3];
-    wfpt_result_poison(poison);
-    const hipError_t e = c->res.p ? hipMemcpyAsync(c->res.p, poison, sizeof(poison),
-                                                    hipMemcpyHostToDevice, c->stream)
-                                  : hipErrorInvalidValue;
+    wfpt::launch_poison(c->ar, c->stream);
+    const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {
       (void)ncclCommAbort(c->comm);
       c->comm = nullptr;
+      if (st.launched) ar_reset(c, d);
       return fail(lrc, lmsg + " (device stream unusable: RCCL communicator aborted; "
                               "re-create it with wfpt_comm_init)");
     }
@@ -1229,12 +1344,52 @@ int wfpt_wiener_like_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params*
   // {sum, zeros, encoded errors} of every rank summed: any zero trial or
   // failure anywhere reaches every rank (wfpt_internal.h: the error counts
   // stay apart under the sum)
-  NCCL_TRY(ncclAllReduce(c->res.p, c->res.p, 3, ncclDouble, ncclSum, c->comm, c->stream));
+  const ncclResult_t nr = ncclAllReduce(c->ar, c->ar, 3, ncclDouble, ncclSum, c->comm, c->stream);
   if (lrc != WFPT_OK) {
     (void)hipStreamSynchronize(c->stream);
+    if (st.launched) ar_reset(c, d);
     return fail(lrc, lmsg);
   }
+  if (nr != ncclSuccess) {
+    if (st.launched) ar_reset(c, d);
+    return fail(WFPT_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+  }
   return ar_finish(c, d, st, out);
+}
+
+int wfpt_wiener_like_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
+                           const wfpt_knobs* k, double triple[3]) {
+  if (!c || !d || !p || !k || !triple) return fail(WFPT_ERR_ARG, "null pointer");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  const wfpt::Params P = to_params(p);
+  const wfpt::Knobs K = to_knobs(k);
+  if (!p_outlier_in_range(P.p_outlier)) {  // -inf on every rank: one zero trial
+    triple[0] = 0.0;
+    triple[1] = 1.0;
+    triple[2] = 0.0;
+    return WFPT_OK;
+  }
+  WFPT_RANGE("wfpt_wiener_like_local");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  ArState st;
+  int rc = ar_launch(c, d, P, K, &st);
+  if (rc == WFPT_OK) rc = ar_settle(c, d, P, K, st);
+  if (rc != WFPT_OK) {
+    ar_reset(c, d);
+    return rc;
+  }
+  double h[8];
+  HIP_TRY(hipMemcpyAsync(h, c->ar, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  split_advance(d, st.eng && !st.lean, h);
+  if (st.eng) note_tree(d, h);
+  d->no_defer = false;
+  (void)finish_profile(c);
+  triple[0] = h[0];
+  triple[1] = h[1];
+  triple[2] = h[2];
+  return WFPT_OK;
 }
 
 int wfpt_wiener_like_allreduce_group(wfpt_ctx* const* ctxs, const wfpt_ds* const* dss, int n,
@@ -1272,7 +1427,7 @@ int wfpt_wiener_like_allreduce_group(wfpt_ctx* const* ctxs, const wfpt_ds* const
   if (rc == WFPT_OK) {
     ncclResult_t r = ncclGroupStart();
     for (int i = 0; i < n && r == ncclSuccess; ++i)
-      r = ncclAllReduce(ctxs[i]->res.p, ctxs[i]->res.p, 3, ncclDouble, ncclSum, ctxs[i]->comm,
+      r = ncclAllReduce(ctxs[i]->ar, ctxs[i]->ar, 3, ncclDouble, ncclSum, ctxs[i]->comm,
                         ctxs[i]->stream);
     const ncclResult_t r2 = ncclGroupEnd();
     if (r == ncclSuccess) r = r2;

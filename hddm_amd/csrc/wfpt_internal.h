@@ -73,7 +73,8 @@ bool has_deferred_pass(const Params& P, const Knobs& K);
 int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 
 // out_kind: 0 = partial {sum, zeros}; 1 = per-trial density (logp => log);
-// 2 = per-trial log p. part: kPassFast (level-0 pass, or the whole fixed
+// 2 = per-trial log p; 3 = 0's partials + each trial's log term in trial[n]
+// (the per-trial check of the summing kernels). part: kPassFast (level-0 pass, or the whole fixed
 // Simpson kernel) | kPassDeferred (the deferred trials + fold). Adaptive
 // families only: kPassLean makes the level-0 pass the lean kernel (level 0
 // without the in-wave refinement; a chunk that refines is flagged in W.redo
@@ -84,7 +85,7 @@ constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPa
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,
-                   const Split* split = nullptr);
+                   const Split* split = nullptr, double* trial = nullptr);
 // out[0..3] = {sum of nb partials, #zero trials, encoded error flags,
 // kResDeferred (defer_bits: some chunk's zero word carries kZeroDefer) |
 // kResTree (*tree_any; then *tree_any = 0)}, out[6] = *tree_any (chunks that
@@ -101,22 +102,28 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer
 // One-block call (n <= 256, direct or adaptive family, level-0 pass + the
 // finalize in one launch: the same result bits and completion word as
 // launch_trials(kPassFast [| kPassLean]) + launch_finalize). false: not
-// eligible, nothing launched.
+// eligible, nothing launched. trial (nullable): out_kind 3's per-trial terms.
 bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                   int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
-                  int* tree_any, hipStream_t s);
+                  int* tree_any, hipStream_t s, double* trial = nullptr);
 // fin (device, 3 * 64 doubles) + ticket (device int, 0 at rest): scratch of the
 // multi-block finalize for large nb (nullptr: one block)
 // res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then
 // out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
+// res[0..2] = wfpt_result_poison's triple {0, 0, kPeerFailUnit}, res[3..7] = 0
+// (one thread, stream order: the all-reduce of a rank whose local pass failed)
+void launch_poison(double* res, hipStream_t s);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
-// two-pass fast path; d_idx / d_par hold up to n deferred trials, *n_defer
-// must be 0 on the stream), or -1 (mixed / fixed Simpson: one generic
-// per-trial kernel with a per-lane mode).
+// two-pass fast path; *n_defer must be 0 on the stream: the direct family's
+// deferred (index, row) records in d_idx / d_par (up to n), the adaptive
+// families' listed chunks in clist (up to (n + 63) / 64)), or -1 (mixed /
+// fixed Simpson: one generic per-trial kernel with a per-lane mode). prof
+// (COUNT builds, evals != null): the node tallies of wfpt_profile_lists.
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
-                  int* n_defer, unsigned long long* evals, int* status, hipStream_t s);
+                  int* n_defer, int* clist, unsigned long long* evals, int* status, int* prof,
+                  hipStream_t s);
 // res (device, n_nodes) per-node sums; then out (mapped host): [0, n_nodes)
 // the sums, [n_nodes] encoded error flags, [n_nodes + 1] the completion word.
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,

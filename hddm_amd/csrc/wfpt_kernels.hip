@@ -57,7 +57,11 @@ struct FastWaves {
 #define WFPT_FOLD_GRID 16384
 #endif
 
-enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2 };
+// OUT_BOTH (the per-trial check of the summing kernels, wfpt_wiener_like_trials):
+// exactly OUT_SUM's chunk partials and zero words, plus each trial's log term
+// (-inf for a zero density) in A.trial[i]: the same template with one more store.
+enum Out : int { OUT_SUM = 0, OUT_ARRAY = 1, OUT_LOGP = 2, OUT_BOTH = 3 };
+constexpr bool sum_out(int out) { return out == OUT_SUM || out == OUT_BOTH; }
 // OUT_SUM per-chunk zero-count word: zero-density trials | kZeroDefer if the
 // chunk's level-0 pass deferred trials (or left the chunk to the redo pass)
 constexpr int kZeroDefer = 1 << 16;
@@ -103,8 +107,9 @@ struct TrialArgs {
   Params P;
   Knobs K;
   double wp_outlier;      // w_outlier * p_outlier
-  double* out;            // OUT_SUM: chunk / block partial sums; OUT_ARRAY/OUT_LOGP: per trial
-  int* zeros;             // OUT_SUM: chunk / block zero counts
+  double* out;            // OUT_SUM/BOTH: chunk / block partial sums; OUT_ARRAY/OUT_LOGP: per trial
+  int* zeros;             // OUT_SUM/BOTH: chunk / block zero counts
+  double* trial;          // OUT_BOTH: per-trial log terms
   unsigned long long* evals;
   int* status;            // error flags (kFlagDepth | kFlagBudget)
   int logp;               // OUT_ARRAY: return log density
@@ -121,6 +126,7 @@ __device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp,
     if (p == 0) zero = 1;
     else lp = log(p);
     if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
+    if (OUT == OUT_BOTH) A.trial[i] = zero ? -INFINITY : lp;
   }
 }
 
@@ -161,7 +167,7 @@ void fast_kernel(TrialArgs A, Work W) {
   if (i < A.n && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
   if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
   const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
-  if (OUT == OUT_SUM) {
+  if (sum_out(OUT)) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
     if (lane == 0) {
@@ -532,7 +538,7 @@ __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, i
   int zero = 0;
   if (i < A.n && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
   const bool anyd = defer_slots(W, c, lane, defer, rf);
-  if (OUT == OUT_SUM) {
+  if (sum_out(OUT)) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
     if (lane == 0) {
@@ -609,7 +615,7 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   const double lpc = S.lp[slot * 64 + lane];
   const int m = S.meta[slot * 64 + lane];
   const bool anyd = defer_slots(W, c, lane, (m >> 1) & 1, m >> 2);
-  if (OUT == OUT_SUM) {
+  if (sum_out(OUT)) {
     const double sum = wave_sum(lpc);
     const int zs = __popcll(__ballot((m & 1) != 0));
     if (lane == 0) {
@@ -817,7 +823,7 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
     if (lane == 0) {
       W.redo[c] = 1;
       // finalize reports the call as deferred: the host runs the redo pass
-      if (OUT == OUT_SUM) A.zeros[c] = kZeroDefer;
+      if (sum_out(OUT)) A.zeros[c] = kZeroDefer;
     }
     return;
   }
@@ -962,7 +968,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, 
         emit<OUT>(A, i, p, lp, zero);
         if (COUNT) atomicAdd(&W.prof[(fl & kFlagExact) ? 5 : 6], 1);
       }
-      if (OUT == OUT_SUM) {
+      if (sum_out(OUT)) {
         lp = wave_sum(lp);
         const int zs = __popcll(__ballot(zero != 0));
         if (lane == 0) {
@@ -995,10 +1001,10 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
     if (flags & kFlagErrors) atomicOr(A.status, flags & kFlagErrors);
     emit<OUT>(A, i, p, lp, zero);
   }
-  if (OUT == OUT_SUM || COUNT) {
+  if (sum_out(OUT) || COUNT) {
     block_reduce<COUNT>(lp, zero, ne);
     if (threadIdx.x == 0) {
-      if (OUT == OUT_SUM) {
+      if (sum_out(OUT)) {
         A.out[blockIdx.x] = lp;
         A.zeros[blockIdx.x] = zero;
       }
@@ -1166,7 +1172,7 @@ struct FinArgs {
   int defer_bits;
 };
 
-template <int MODE>
+template <int MODE, int OUT>
 __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, RootGrids R,
                                                            FinArgs F) {
   __shared__ double fp[kFastBlock / 64];
@@ -1188,7 +1194,7 @@ __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, 
       if (own) oc = fast_level0<MODE>(A.x[i], A.P, A.K, p, f0, ne0, flags, pend0);
       double lp = 0.0;
       int zero = 0;
-      if (own && oc == kFinal) emit<OUT_SUM>(A, i, p, lp, zero);
+      if (own && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
       const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
       part = wave_sum(lp);
       zw = __popcll(__ballot(zero != 0)) | (anyd ? kZeroDefer : 0);
@@ -1216,7 +1222,7 @@ __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, 
         double lp = 0.0;
         int zero = 0;
         const bool defer = oc == kExact;
-        if (own && !defer) emit<OUT_SUM>(A, i, p, lp, zero);
+        if (own && !defer) emit<OUT>(A, i, p, lp, zero);
         const bool anyd = defer_slots(W, c, lane, defer, kFlagExact);
         part = wave_sum(lp);
         zw = __popcll(__ballot(zero != 0)) | (anyd ? kZeroDefer : 0);
@@ -1277,6 +1283,14 @@ __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* 
 
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s) {
   hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(64), 0, s, res, out, seq);
+}
+
+__global__ __launch_bounds__(64) void poison_kernel(double* res) {
+  if (threadIdx.x < 8) res[threadIdx.x] = threadIdx.x == 2 ? kPeerFailUnit : 0.0;
+}
+
+void launch_poison(double* res, hipStream_t s) {
+  hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(64), 0, s, res);
 }
 
 // One wave per node: sums per-trial log p of [off[j], off[j+1]) in fixed order.
@@ -1372,15 +1386,17 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(
 // Two-pass per-node path (used when every node's parameters select the same
 // integration family, the usual HDDM case: sv/sz/st are group-level):
 // node_fast_kernel is the level-0 pass with the node's parameter row (staged
-// in LDS as in node_kernel) and per-trial log p out; a trial that needs
-// refinement or the exact path is appended — index and parameter row — to a
-// dense deferred list (wave-aggregated atomic; outputs are per trial, so the
-// order does not matter), which node_slow_kernel runs 64 trials per wave.
+// in LDS as in node_kernel) and per-trial log p out. Adaptive families: a wave
+// (64 consecutive stored trials: a chunk) with a trial that needs refinement
+// or the exact path appends its chunk id to a dense list (one atomic per
+// wave), which node_chunk_kernel completes 64 trials per wave. Direct family:
+// the rare exact-path trials are appended as (index, parameter row) records
+// for node_slow_kernel.
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
-                      double* lp, int64_t* d_idx, Params* d_par, int* n_defer,
-                      unsigned long long* evals, int* status) {
+                      double* lp, int64_t* d_idx, Params* d_par, int* n_defer, int* clist,
+                      int* n_chunks, unsigned long long* evals, int* status, int* prof) {
   __shared__ Params rows[kStageRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
   const int64_t i = i0 + threadIdx.x;
@@ -1410,18 +1426,149 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   }
   const unsigned long long b = __ballot(defer);
   if (b) {
-    int base = 0;
-    if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
-    base = __shfl(base, 0, 64);
-    if (defer) {
-      const int k = base + __popcll(b & lanemask_lt(lane));
-      d_idx[k] = i;
-      d_par[k] = Q;
+    if (MODE == kDirect) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
+      base = __shfl(base, 0, 64);
+      if (defer) {
+        const int k = base + __popcll(b & lanemask_lt(lane));
+        d_idx[k] = i;
+        d_par[k] = Q;
+      }
+    } else if (lane == 0) {
+      clist[atomicAdd(n_chunks, 1)] = (int)(i >> 6);
     }
   }
   if (COUNT) {
     ne = wave_sum_ll(defer ? 0 : ne);
-    if (lane == 0) atomicAdd(evals, (unsigned long long)ne);
+    if (lane == 0) {
+      atomicAdd(evals, (unsigned long long)ne);
+      if (b) atomicAdd(&prof[3], __popcll(b));
+    }
+  }
+}
+
+// The node path's completion of the chunks node_fast_kernel listed: one wave
+// per chunk, as the dataset engine (engine_kernel) runs a chunk, per node
+// segment of the chunk (nodes are contiguous and |rt|-ordered: a chunk holds
+// one node, or the end of one and the start of the next). Per segment: the
+// node's parameter row (wave-uniform), its tables built by the lanes in
+// parallel into the wave's LDS (eng_tables_wave), level 0 per lane on the
+// segment's trials, the in-wave refinement rounds over all of them together,
+// then each trial's density (tree17 over its values; the exact path or the
+// per-lane walk for the rare trials the rounds hand on) and its term. Every
+// trial of a listed chunk is rewritten (the same level-0 operations as the
+// fast pass), so a chunk's terms do not depend on which lanes deferred.
+// Replaces one wave per deferred trial: a call where most trials refine (an
+// MCMC proposal far in the tails) runs 64 trials per wave.
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
+    const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
+    const int* clist, const int* n_chunks, unsigned long long* evals, int* status, int* prof) {
+  __shared__ ChunkLds<1> lds[kEngWaves];
+  const int lane = threadIdx.x & 63;
+  ChunkLds<1>& cl = lds[threadIdx.x >> 6];
+  const int nc = *n_chunks;
+  const int nwaves = (int)gridDim.x * kEngWaves;
+  long long ne = 0;
+  int errf = 0, nseg = 0, nex = 0, nwk = 0;
+  Tally ty;
+  for (int k = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
+       k < nc; k += nwaves) {
+    const int64_t c = clist[k];
+    const int64_t i = c * 64 + lane;
+    const bool own = i < n;
+    const double x0 = own ? x[i] : 0.0;
+    const int nj = own ? node[i] : -1;
+    bool todo = own;
+    for (unsigned long long left = __ballot(todo); left; left = __ballot(todo)) {
+      // the next node segment: the node of the first lane still to do
+      const int jn = __shfl(nj, __ffsll((long long)left) - 1, 64);
+      const bool mine = todo && nj == jn;
+      todo = todo && !mine;
+      ++nseg;
+      const Params Q = P[__builtin_amdgcn_readfirstlane(jn)];
+      TrialArgs A{};
+      A.x = x;
+      A.n = n;
+      A.P = Q;
+      A.K = K;
+      A.wp_outlier = K.w_outlier * Q.p_outlier;
+      eng_tables_wave(Q, cl.tab, lane);
+      double p = 0.0, f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      long long ne0 = 0;
+      unsigned pend0 = 0u;
+      int oc = kFinal;
+      if (mine) oc = eng_level0<MODE>(x0, Q, K, cl.tab.G[x0 > 0][kGridRoot], p, f0, ne0, pend0);
+      if (__ballot(mine && oc == kTree) != 0ull) {
+        cl.X[lane] = x0;
+        cl.fl[lane] = (mine && oc == kTree) ? 0 : (mine && oc == kExact ? (int)kFlagExact
+                                                                         : (int)kFlagIdle);
+        if (COUNT) cl.cnt[lane] = (int)ne0;
+        if (mine && oc == kTree) {
+#pragma unroll
+          for (int j = 0; j < 5; ++j) cl.F[j * (kTreeW / 4) * 64 + lane] = f0[j];
+        }
+        if (lane == 0) {
+          cl.qn[0] = 0;
+          cl.qn[1] = 0;
+        }
+        wave_sync();
+        if (MODE == kAdaptTZ) {
+#pragma unroll
+          for (int j = 0; j < 5; ++j)
+            team_push(mine && oc == kTree && ((pend0 >> (j * (kTreeW / 4))) & 1u),
+                      lane | ((j * (kTreeW / 4)) << 6), cl.ZQ, &cl.qn[1]);
+        }
+        wave_sync();
+        PhaseClock pc;
+        Tally t1;
+        refine_rounds<MODE, COUNT, 1>(A, cl, lane, 1, t1, pc);
+        if (COUNT) {
+          ty.t1 += t1.t1;
+          ty.t2 += t1.t2;
+          ty.rec += t1.rec;
+          for (int q = 0; q < 3; ++q) ty.z[q] += t1.z[q];
+        }
+      }
+      bool defer = mine && oc == kExact;
+      int rf = kFlagExact;
+      long long n1 = ne0;
+      if (mine && oc == kTree) {
+        tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+        if (COUNT) n1 = cl.cnt[lane];
+      }
+      if (defer) {
+        n1 = 0;
+        if (COUNT) ++((rf & kFlagExact) ? nex : nwk);
+        p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
+                              : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+      }
+      if (mine) {
+        ne += n1;
+        lp[i] = node_logp(p, Q, K);
+      }
+      wave_sync();  // the next segment rebuilds this wave's LDS
+    }
+  }
+  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
+  if (COUNT) {
+    ne = wave_sum_ll(ne);
+    nex = (int)wave_sum_ll(nex);
+    nwk = (int)wave_sum_ll(nwk);
+    if (lane == 0) {
+      atomicAdd(evals, (unsigned long long)ne);
+      atomicAdd(&prof[0], nseg);
+      atomicAdd(&prof[5], nex);
+      atomicAdd(&prof[6], nwk);
+      atomicAdd(&prof[1], ty.t1);
+      atomicAdd(&prof[2], ty.t2);
+      atomicAdd(&prof[4], ty.rec);
+      atomicAdd(&prof[7], ty.z[0] + ty.z[1] + ty.z[2]);
+      atomicAdd(&prof[8], ty.z[0]);
+      atomicAdd(&prof[9], ty.z[1]);
+      atomicAdd(&prof[10], ty.z[2]);
+    }
   }
 }
 
@@ -1584,7 +1731,7 @@ __global__ __launch_bounds__(kBlock) void lp_sum_kernel(const double* lp, int64_
 
 static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const Knobs& K,
                             double* out, int* zeros, unsigned long long* evals, int* status,
-                            int logp) {
+                            int logp, double* trial = nullptr) {
   TrialArgs A;
   A.x = x;
   A.n = n;
@@ -1596,6 +1743,7 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
   A.evals = evals;
   A.status = status;
   A.logp = logp;
+  A.trial = trial;
   return A;
 }
 
@@ -1685,12 +1833,16 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done,
-                   const Split* split) {
+                   const Split* split, double* trial) {
   if (n <= 0) return;
   Split S{};
   if (split) S = *split;
-  const TrialArgs A = trial_args(x, n, P, K, out, zeros, evals, status, logp);
+  const TrialArgs A = trial_args(x, n, P, K, out, zeros, evals, status, logp, trial);
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
+  if (out_kind == OUT_BOTH) {  // the per-trial check (no evaluation counting)
+    launch_mode<false, OUT_BOTH>(mode, part, A, W, S, s, fast_done);
+    return;
+  }
   if (evals) {
     if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, S, s, fast_done);
     else if (out_kind == OUT_ARRAY)
@@ -1706,30 +1858,41 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
 
 bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                   int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
-                  int* tree_any, hipStream_t s) {
+                  int* tree_any, hipStream_t s, double* trial) {
   if (n <= 0 || n > kFastBlock) return false;
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   if (mode > kAdaptTZ) return false;
-  const TrialArgs A = trial_args(x, n, P, K, part, zeros, nullptr, status, 0);
+  const TrialArgs A = trial_args(x, n, P, K, part, zeros, nullptr, status, 0, trial);
   Work F = W;
   F.redo = mode == kDirect ? nullptr : W.redo;
   RootGrids R{};
   if (mode != kDirect) root_grids(P, R);
   const FinArgs Fa{status, out, seq, tree_any, 1};
-  switch (mode) {
-    case kDirect:
-      hipLaunchKernelGGL(small_kernel<kDirect>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
-      break;
-    case kAdaptT:
-      hipLaunchKernelGGL(small_kernel<kAdaptT>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
-      break;
-    case kAdaptZ:
-      hipLaunchKernelGGL(small_kernel<kAdaptZ>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
-      break;
-    default:
-      hipLaunchKernelGGL(small_kernel<kAdaptTZ>, dim3(1), dim3(kFastBlock), 0, s, A, F, R, Fa);
-      break;
+#define SMALL_MODES(O_)                                                                      \
+  switch (mode) {                                                                            \
+    case kDirect:                                                                            \
+      hipLaunchKernelGGL((small_kernel<kDirect, O_>), dim3(1), dim3(kFastBlock), 0, s, A, F, R, \
+                         Fa);                                                                \
+      break;                                                                                 \
+    case kAdaptT:                                                                            \
+      hipLaunchKernelGGL((small_kernel<kAdaptT, O_>), dim3(1), dim3(kFastBlock), 0, s, A, F, R, \
+                         Fa);                                                                \
+      break;                                                                                 \
+    case kAdaptZ:                                                                            \
+      hipLaunchKernelGGL((small_kernel<kAdaptZ, O_>), dim3(1), dim3(kFastBlock), 0, s, A, F, R, \
+                         Fa);                                                                \
+      break;                                                                                 \
+    default:                                                                                 \
+      hipLaunchKernelGGL((small_kernel<kAdaptTZ, O_>), dim3(1), dim3(kFastBlock), 0, s, A, F,   \
+                         R, Fa);                                                             \
+      break;                                                                                 \
   }
+  if (trial) {
+    SMALL_MODES(OUT_BOTH)
+  } else {
+    SMALL_MODES(OUT_SUM)
+  }
+#undef SMALL_MODES
   return true;
 }
 
@@ -1748,15 +1911,18 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer
 template <int MODE, bool COUNT>
 static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t n,
                                   const Params* P, const Knobs& K, double* lp, int64_t* d_idx,
-                                  Params* d_par, int* n_defer, unsigned long long* evals,
-                                  int* status, hipStream_t s) {
+                                  Params* d_par, int* n_defer, int* clist,
+                                  unsigned long long* evals, int* status, int* prof,
+                                  hipStream_t s) {
   hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
-                     node, n, P, K, lp, d_idx, d_par, n_defer, evals, status);
+                     node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
+                     prof);
   if constexpr (MODE != kDirect) {
-    // adaptive families: one wave per deferred record (node_engine_kernel)
-    const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 1024);
-    hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, false>), dim3(nb), dim3(kEngBlock), 0, s, x,
-                       K, lp, d_idx, d_par, n_defer, evals, status);
+    // adaptive families: one wave per listed chunk (node_chunk_kernel)
+    const int64_t nw = (n + 63) / 64;
+    const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
+    hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
+                       n, P, K, lp, clist, n_defer, evals, status, prof);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;
@@ -1769,10 +1935,11 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
 template <bool COUNT>
 static void launch_nodes_mode(int mode, const double* x, const int32_t* node, int64_t n,
                               const Params* P, const Knobs& K, double* lp, int64_t* d_idx,
-                              Params* d_par, int* n_defer, unsigned long long* evals,
-                              int* status, hipStream_t s) {
-#define TWO_PASS(M_) \
-  launch_nodes_two_pass<M_, COUNT>(x, node, n, P, K, lp, d_idx, d_par, n_defer, evals, status, s)
+                              Params* d_par, int* n_defer, int* clist,
+                              unsigned long long* evals, int* status, int* prof, hipStream_t s) {
+#define TWO_PASS(M_)                                                                           \
+  launch_nodes_two_pass<M_, COUNT>(x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, evals,  \
+                                   status, prof, s)
   switch (mode) {
     case kDirect: TWO_PASS(kDirect); break;
     case kAdaptT: TWO_PASS(kAdaptT); break;
@@ -1784,15 +1951,17 @@ static void launch_nodes_mode(int mode, const double* x, const int32_t* node, in
 
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
-                  int* n_defer, unsigned long long* evals, int* status, hipStream_t s) {
+                  int* n_defer, int* clist, unsigned long long* evals, int* status, int* prof,
+                  hipStream_t s) {
   const int64_t nb = blocks_for(n);
   if (nb == 0) return;
   if (mode >= kDirect && mode <= kAdaptTZ) {
     if (evals)
-      launch_nodes_mode<true>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, evals, status, s);
+      launch_nodes_mode<true>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, evals,
+                              status, prof, s);
     else
-      launch_nodes_mode<false>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, evals, status,
-                               s);
+      launch_nodes_mode<false>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, evals,
+                               status, prof, s);
     return;
   }
   const int stk = stack_kind(K);

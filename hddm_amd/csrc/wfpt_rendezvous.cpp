@@ -1,12 +1,16 @@
 // wfpt_rendezvous.cpp — torch-free exchange of the RCCL unique id (128 bytes)
 // between the ranks of one job over TCP (POSIX sockets only).
 //
-// Rank 0 listens on (host, port) and sends its 128-byte id to each of the
-// nranks - 1 peers that connect; every other rank connects (retrying until
-// the deadline: rank 0 may start later) and reads the id. A peer identifies
+// Rank 0 listens on the wildcard address of host's family at `port` (so peers
+// reach it whatever address the name resolves to locally, e.g. 127.0.1.1 from
+// /etc/hosts) and sends its 128-byte id to each of the nranks - 1 peers that
+// connect; every other rank connects (non-blocking, retrying until the
+// deadline: rank 0 may start later) and reads the id. A peer identifies
 // itself with a 16-byte hello {magic, nranks, rank} that rank 0 checks, so a
 // stray connection or a job with another world size is rejected instead of
-// silently joining. Nothing here touches the GPU.
+// silently joining, and acknowledges the id with one byte: rank 0 counts a
+// peer as served only after its ack (a peer whose read failed reconnects).
+// Nothing here touches the GPU.
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -32,6 +36,7 @@ int wfpt_rdv_fail(int code, const std::string& msg);  // wfpt_capi.cpp (last-err
 namespace {
 
 constexpr uint32_t kMagic = 0x77667074u;  // "wfpt"
+constexpr unsigned char kAck = 0x5a;
 using Clock = std::chrono::steady_clock;
 
 struct Fd {
@@ -79,6 +84,45 @@ bool resolve(const char* host, int port, sockaddr_storage* sa, socklen_t* len) {
   return true;
 }
 
+// The wildcard address of family `fam` at `port` (rank 0's listening socket).
+socklen_t wildcard(int fam, int port, sockaddr_storage* sa) {
+  std::memset(sa, 0, sizeof(*sa));
+  if (fam == AF_INET6) {
+    auto* s6 = reinterpret_cast<sockaddr_in6*>(sa);
+    s6->sin6_family = AF_INET6;
+    s6->sin6_addr = in6addr_any;
+    s6->sin6_port = htons((uint16_t)port);
+    return sizeof(sockaddr_in6);
+  }
+  auto* s4 = reinterpret_cast<sockaddr_in*>(sa);
+  s4->sin_family = AF_INET;
+  s4->sin_addr.s_addr = htonl(INADDR_ANY);
+  s4->sin_port = htons((uint16_t)port);
+  return sizeof(sockaddr_in);
+}
+
+// Non-blocking connect polled against the deadline (an unreachable host
+// cannot stall the caller past it). Leaves fd non-blocking (io_all polls).
+bool connect_by(int fd, const sockaddr_storage& sa, socklen_t len, Clock::time_point deadline) {
+  const int fl = ::fcntl(fd, F_GETFL, 0);
+  if (fl < 0 || ::fcntl(fd, F_SETFL, fl | O_NONBLOCK) != 0) return false;
+  if (::connect(fd, (const sockaddr*)&sa, len) == 0) return true;
+  if (errno != EINPROGRESS && errno != EINTR) return false;
+  for (;;) {
+    pollfd q{fd, POLLOUT, 0};
+    const int t = ms_left(deadline);
+    if (t == 0) return false;
+    const int pr = ::poll(&q, 1, t < 200 ? t : 200);
+    if (pr < 0 && errno == EINTR) continue;
+    if (pr < 0) return false;
+    if (pr == 0) continue;
+    int err = 0;
+    socklen_t el = sizeof(err);
+    if (::getsockopt(fd, SOL_SOCKET, SO_ERROR, &err, &el) != 0) return false;
+    return err == 0;
+  }
+}
+
 }  // namespace
 
 extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int port,
@@ -92,15 +136,16 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
   if (!resolve(host, port, &sa, &slen))
     return wfpt_rdv_fail(WFPT_ERR_COMM, std::string("rendezvous: cannot resolve ") + host);
   if (rank == 0) {
+    sockaddr_storage la{};
+    const socklen_t llen = wildcard(sa.ss_family, port, &la);
     Fd ls;
-    ls.fd = ::socket(sa.ss_family, SOCK_STREAM, 0);
+    ls.fd = ::socket(la.ss_family, SOCK_STREAM, 0);
     if (ls.fd < 0) return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: socket() failed");
     const int one = 1;
     (void)::setsockopt(ls.fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    if (::bind(ls.fd, (sockaddr*)&sa, slen) != 0 || ::listen(ls.fd, nranks) != 0)
-      return wfpt_rdv_fail(WFPT_ERR_COMM, std::string("rendezvous: cannot listen on ") + host +
-                                              ":" + std::to_string(port) + " (" +
-                                              strerror(errno) + ")");
+    if (::bind(ls.fd, (sockaddr*)&la, llen) != 0 || ::listen(ls.fd, nranks) != 0)
+      return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: cannot listen on port " +
+                                              std::to_string(port) + " (" + strerror(errno) + ")");
     std::vector<bool> seen(nranks, false);
     for (int got = 0; got < nranks - 1;) {
       pollfd q{ls.fd, POLLIN, 0};
@@ -110,7 +155,7 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
       if (pr <= 0)
         return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: timed out with " + std::to_string(got) +
                                                 " of " + std::to_string(nranks - 1) +
-                                                " peers connected");
+                                                " peers served");
       Fd c;
       c.fd = ::accept(ls.fd, nullptr, nullptr);
       if (c.fd < 0) continue;
@@ -120,9 +165,12 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
       if (hello[0] != kMagic || (int)hello[1] != nranks || pr_rank <= 0 || pr_rank >= nranks ||
           seen[pr_rank])
         continue;  // not one of this job's peers: ignored
-      if (!io_all(c.fd, id, 128, true, deadline))
-        return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: sending the id to rank " +
-                                                std::to_string(pr_rank) + " failed");
+      unsigned char ack = 0;
+      // served only once the peer confirms it holds the id (otherwise it
+      // reconnects and is served again)
+      if (!io_all(c.fd, id, 128, true, deadline) || !io_all(c.fd, &ack, 1, false, deadline) ||
+          ack != kAck)
+        continue;
       seen[pr_rank] = true;
       ++got;
     }
@@ -132,11 +180,12 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
     Fd c;
     c.fd = ::socket(sa.ss_family, SOCK_STREAM, 0);
     if (c.fd < 0) return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: socket() failed");
-    if (::connect(c.fd, (sockaddr*)&sa, slen) == 0) {
+    if (connect_by(c.fd, sa, slen, deadline)) {
       const uint32_t hello[4] = {kMagic, (uint32_t)nranks, (uint32_t)rank, 0};
       unsigned char buf[128];
+      unsigned char ack = kAck;
       if (io_all(c.fd, (void*)hello, sizeof(hello), true, deadline) &&
-          io_all(c.fd, buf, 128, false, deadline)) {
+          io_all(c.fd, buf, 128, false, deadline) && io_all(c.fd, &ack, 1, true, deadline)) {
         std::memcpy(id, buf, 128);
         return WFPT_OK;
       }

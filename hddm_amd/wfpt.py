@@ -223,6 +223,40 @@ class Dataset:
                                          ctypes.byref(K), ctypes.byref(out)))
         return out.value
 
+    def wiener_like_trials(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10, use_adaptive=1,
+                           simps_err=1e-8, p_outlier=0, w_outlier=0.1):
+        """wiener_like plus each trial's addend (wfpt.pyx:66-74), in the order the
+        trials were given: (total, terms). Same call sequence and kernels as
+        wiener_like (with one more store per trial): the per-trial check of the
+        summing path."""
+        P = _lib.make_params(v, sv, a, z, sz, t, st, p_outlier)
+        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        out = ctypes.c_double()
+        terms = np.empty(self.n, dtype=np.float64)
+        _lib.check(_lib.wfpt_wiener_like_trials(self.ctx.handle, self.handle, ctypes.byref(P),
+                                                ctypes.byref(K), ctypes.byref(out),
+                                                _lib.dptr(terms)))
+        return out.value, terms
+
+    def order(self):
+        """order()[i] = the caller's index of stored trial i (chunk c holds
+        stored trials 64c .. 64c + 63)."""
+        perm = np.empty(self.n, dtype=np.int64)
+        _lib.check(_lib.wfpt_dataset_order(self.handle,
+                                           perm.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+        return perm
+
+    def local_triple(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10, use_adaptive=1,
+                     simps_err=1e-8, p_outlier=0, w_outlier=0.1):
+        """This shard's {sum log p, #zero trials, encoded errors}: what
+        wiener_like_allreduce contributes to its all-reduce."""
+        P = _lib.make_params(v, sv, a, z, sz, t, st, p_outlier)
+        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        r = (ctypes.c_double * 3)()
+        _lib.check(_lib.wfpt_wiener_like_local(self.ctx.handle, self.handle, ctypes.byref(P),
+                                               ctypes.byref(K), r))
+        return [r[0], r[1], r[2]]
+
     def wiener_like_allreduce(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10,
                               use_adaptive=1, simps_err=1e-8, p_outlier=0, w_outlier=0.1):
         """Global sum over every rank's shard (requires hddm_amd.dist.init_comm; torch-free)."""

@@ -96,6 +96,19 @@ void wfpt_shard_range(int64_t n, int nranks, int rank, int64_t *lo, int64_t *hi)
 /* Sum of log mixture densities over a resident dataset (wfpt.pyx:54-76). */
 int wfpt_wiener_like(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
                      const wfpt_knobs *k, double *out_logp);
+/* wfpt_wiener_like with each trial's addend of the sum too (the
+ * `log(p * (1 - p_outlier) + wp_outlier)` terms of wfpt.pyx:66-74; -inf for a
+ * zero mixture density) in out_trial[n], in the caller's trial order. It takes
+ * the same predicted call sequence (lean level-0 pass, one-launch small path,
+ * engine, redo, fold) as wfpt_wiener_like would, with the same kernels built
+ * with one extra store per trial, and leaves the same chunk partials: the
+ * per-trial check of the summing path (tests), not a hot-path call. */
+int wfpt_wiener_like_trials(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
+                            const wfpt_knobs *k, double *out_logp, double *out_trial);
+/* perm[i] = the caller's index of the dataset's stored trial i (datasets are
+ * stored grouped by node / boundary and ordered by |rt|; identity for
+ * WFPT_DS_INPUT_ORDER). */
+int wfpt_dataset_order(const wfpt_ds *ds, int64_t *perm);
 /* Same on a host array (uploaded for this call). */
 int wfpt_wiener_like_host(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
                           const wfpt_knobs *k, double *out_logp);
@@ -166,11 +179,16 @@ int wfpt_comm_init_tcp(wfpt_ctx *ctx, int nranks, int rank, const char *host, in
  * ncclAllReduce of 3 doubles {sum log p, #zero-density trials, encoded error
  * counts}; every rank receives the global total (-inf if any rank holds a
  * zero-density trial) or every rank fails: WFPT_ERR_UNSUPPORTED if some rank
- * exceeded the depth / evaluation limits; a rank whose local pass failed
- * returns its own error after entering the exchange with a poisoned triple
- * (wfpt_result_poison), and its peers return WFPT_ERR_COMM — no rank is left
- * waiting in the collective. A broken device stream (sticky fault) cannot
- * enter it: that rank aborts its communicator. */
+ * exceeded the depth / evaluation limits; a rank whose call fails after its
+ * communicator exists (bad dataset or pointer arguments, workspace allocation,
+ * a kernel or timeout error in its local pass) returns its own error after
+ * entering the exchange with a poisoned triple (wfpt_result_poison, written on
+ * the device into a triple allocated at wfpt_open), and its peers return
+ * WFPT_ERR_COMM — no rank is left waiting in the collective. Not covered: a
+ * context without a communicator (no collective exists), and a broken device
+ * stream (sticky fault), which cannot enqueue the exchange: that rank aborts
+ * its communicator, and its peers' collective fails or times out in RCCL. A
+ * failed call resets the dataset's call-sequence predictions. */
 int wfpt_wiener_like_allreduce(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
                                const wfpt_knobs *k, double *out_logp);
 /* One process driving n GPUs (e.g. a single PyMC sampler): ctxs[i] (distinct
@@ -182,6 +200,13 @@ int wfpt_comm_init_all(wfpt_ctx *const *ctxs, int n);
 int wfpt_wiener_like_allreduce_group(wfpt_ctx *const *ctxs, const wfpt_ds *const *dss, int n,
                                      const wfpt_params *p, const wfpt_knobs *k,
                                      double *out_logp);
+/* This rank's local triple {sum log p, #zero-density trials, encoded error
+ * counts} of its resident shard — exactly what wfpt_wiener_like_allreduce
+ * contributes to its all-reduce — for a caller that combines shards with its
+ * own collective (sum the triples, then wfpt_decode_result). A p_outlier
+ * outside [0, 1] gives {0, 1, 0} (decodes to -inf). */
+int wfpt_wiener_like_local(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
+                           const wfpt_knobs *k, double triple[3]);
 /* The triple a rank that failed before the exchange contributes: {0, 0,
  * 2^40} (one "failed rank" unit; see wfpt_decode_result). */
 int wfpt_result_poison(double r[3]);
@@ -215,12 +240,31 @@ int wfpt_profile_read(wfpt_ctx *ctx, double *kernel_ms, int64_t *launches, int64
  * refined, counts[5] trials settled on the exact path, counts[6] trials
  * continued on the per-lane walk, counts[7] z walks (counts[8 + L]: at tree
  * level L). counts[11..15]: per-phase engine time of diagnostic builds
- * (WFPT_PHASE_TIMING), kilo-cycles summed over waves. */
+ * (WFPT_PHASE_TIMING), kilo-cycles summed over waves. The per-node path
+ * (wfpt_wiener_like_nodes, adaptive families) adds to the same counters, plus
+ * counts[3] trials its level-0 pass left to the chunk engine and counts[0]
+ * node segments the chunk engine ran (one per node present in a listed
+ * chunk). */
 int wfpt_profile_lists(wfpt_ctx *ctx, int64_t counts[16], int reset);
 /* Diagnostic builds (WFPT_PHASE_TIMING): the last engine launch's per-wave
  * records, 8 words per 64-trial chunk {start, end (100 MHz real-time clock),
  * 5 phase cycle counts, z rounds | t rounds << 32}; zeros otherwise. */
 int wfpt_debug_waves(wfpt_ctx *ctx, uint64_t *out, int64_t max_records);
+/* The first n per-chunk partials {sum of the chunk's log terms, zero word}
+ * the last summing call left on the device (64 stored trials per chunk for
+ * the adaptive / direct families; synchronises the stream). Tests compare
+ * them with the reference's per-chunk sums. */
+int wfpt_debug_partials(wfpt_ctx *ctx, double *part, int32_t *zero, int64_t n);
+/* Kernels the last likelihood call launched (OR of WFPT_PATH_*). */
+#define WFPT_PATH_LEAN 1     /* lean level-0 pass (lean_kernel) */
+#define WFPT_PATH_ENGINE 2   /* in-wave adaptive engine over every chunk */
+#define WFPT_PATH_SMALL 4    /* one-block level 0 + finalize (small_kernel) */
+#define WFPT_PATH_REDO 8     /* engine over the chunks the lean pass flagged */
+#define WFPT_PATH_FOLD 16    /* deferred trials (exact path / deep trees) */
+#define WFPT_PATH_DIRECT 32  /* simple-DDM level 0 (fast_kernel) */
+#define WFPT_PATH_FIXED 64   /* fixed Simpson (trial_kernel) */
+#define WFPT_PATH_SPLIT 128  /* heavy chunks split into one-wave units */
+int wfpt_last_path(wfpt_ctx *ctx, int *path);
 int wfpt_synchronize(wfpt_ctx *ctx);
 
 #ifdef __cplusplus

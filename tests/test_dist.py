@@ -64,11 +64,40 @@ def _worker(rank, world, port, x, args, kn, inject, out_q):
     dist.destroy_process_group()
 
 
-def _run(x, args, kn, inject):
+def _device_worker(rank, world, port, x, args, kn, seq, out_q):
+    """A rank whose triple is the library's own: its contiguous shard resident
+    on the GPU and wfpt_wiener_like_local (the triple wiener_like_allreduce
+    puts into its ncclAllReduce), summed over gloo, decoded by the library."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from hddm_amd import _lib, wfpt
+    from hddm_amd import dist as hdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = hdist.shard_range(x.size, world, rank)
+    ds = wfpt.Dataset(x[lo:hi])
+    res = []
+    for p in seq:  # lean / engine / mispredicted sequences on each rank's own history
+        triple = ds.local_triple(*p, *kn)
+        t = torch.tensor(triple, dtype=torch.float64)
+        dist.all_reduce(t)
+        res.append(_lib.decode_result(t.tolist()))
+    out_q.put((rank, res, hi - lo))
+    ds.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _run(x, args, kn, inject, worker=None, extra=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, x, args, kn, inject, q))
+    if worker is None:
+        worker, extra = _worker, inject
+    procs = [ctx.Process(target=worker, args=(r, 2, port, x, args, kn, extra, q))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -285,3 +314,29 @@ def test_single_process_group_allreduce(gpu, oracle_lib):
     x2 = x.copy()
     x2[-1] = 0.1  # zero density on the last shard
     assert grp.wiener_like(grp.shards(x2), *args, 1e-4, 2, 2, 1, 1e-3, 0.0, 0.1) == -math.inf
+
+
+@pytest.mark.gpu
+def test_two_rank_gloo_with_device_triples(gpu, oracle_lib):
+    """World-2 gloo on the single-GPU lease, each rank a process with its own
+    context on the device: the per-rank triple is the library's (its shard's
+    level-0 / engine / redo passes and finalize, wfpt_wiener_like_local), not
+    the oracle's. The decoded sum equals the unsharded reference on every rank
+    for a call sequence that takes the lean prediction, a misprediction onto
+    refining parameters and back, and a zero-density trial (-inf)."""
+    np.random.seed(12)
+    calm = (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1)
+    heavy = (1.7431, 2.0137, 0.6119, 0.5386, 0.2108, 0.3567, 0.1981)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+    x = gpu.gen_rts_from_cdf(*heavy, samples=60_001, dt=1e-3)
+    seq = [calm, calm, heavy, heavy, calm]
+    res = _run(x, None, kn, None, worker=_device_worker, extra=seq)
+    for r, p in enumerate(seq):
+        terms = oracle_lib.pdf_array(x, *p, kn[0], 1, *kn[1:])
+        ref = math.fsum(terms)
+        for got in res:
+            assert abs(got[r] - ref) <= 1e-11 * math.fsum(np.abs(terms)), (r, got[r], ref)
+    x0 = x.copy()
+    x0[-5] = 0.05  # below t - st/2 on rank 1: -inf everywhere
+    res0 = _run(x0, None, kn, None, worker=_device_worker, extra=[calm])
+    assert all(g[0] == -math.inf for g in res0)
