@@ -138,6 +138,7 @@ struct wfpt_ctx {
   DevBuf<int> wl_n;          // per chunk: deferred trials
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
   DevBuf<unsigned char> redo;  // per chunk: the lean pass left it to the engine (0 at rest)
+  DevBuf<double> st;         // per chunk: level-0 state of the state sequence (kPassState)
   int* tree_any = nullptr;   // device: some chunk refined in-wave (finalize reports + clears)
   double* fin = nullptr;     // device: multi-block finalize scratch (3 x 64 doubles)
   int* fin_ticket = nullptr; // device: its last-block ticket (0 at rest)
@@ -147,7 +148,7 @@ struct wfpt_ctx {
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
   DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
-  int* n_defer = nullptr;    // device: deferred count of the per-node fast path (0 at rest)
+  int* n_defer = nullptr;    // device [2]: deferred counts of the per-node fast path (0 at rest)
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
@@ -161,6 +162,7 @@ struct wfpt_ctx {
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
   bool small = true;           // WFPT_SMALL=0: one-block calls keep the separate finalize
+  bool state = false;          // WFPT_STATE=1: refining calls hand level 0 from the lean pass to the engine
   // WFPT_LEAN_TREE: the largest fraction of refining chunks (last call) for
   // which the lean pass + engine redo of those chunks beats the engine over
   // every chunk
@@ -296,6 +298,9 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   W->prof = c->prof;
   W->phase = c->phase;
   W->nslots = ns;
+  W->st = nullptr;
+  W->pred = nullptr;
+  W->next_pred = nullptr;
   return WFPT_OK;
 }
 
@@ -374,6 +379,12 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   wfpt::Work W;
   if (int rc = reserve_work(c, n, &W)) return rc;
   const bool adaptive = wfpt::has_deferred_pass(P, K);
+  if ((part & wfpt::kPassState) && engine_family(P, K)) {
+    HIP_TRY(c->st.reserve((size_t)((n + 63) / 64) * 64 * wfpt::kStateWords));
+    W.st = c->st.p;
+  } else {
+    part &= ~wfpt::kPassState;
+  }
   if (part & wfpt::kPassFast) c->path = 0;  // a call sequence starts
   if (c->count && (part & wfpt::kPassFast))
     HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
@@ -407,10 +418,12 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   } else {
     if (part & wfpt::kPassFast)
       c->path |= direct ? WFPT_PATH_DIRECT
-                        : (part & wfpt::kPassLean)
+                        : (part & (wfpt::kPassLean | wfpt::kPassState))
                               ? WFPT_PATH_LEAN
                               : (WFPT_PATH_ENGINE | (S.n > 0 ? WFPT_PATH_SPLIT : 0));
     if (!direct && (part & wfpt::kPassRedo)) c->path |= WFPT_PATH_REDO;
+    if (part & wfpt::kPassState)
+      c->path |= WFPT_PATH_STATE | ((part & wfpt::kPassDeferred) && S.n > 0 ? WFPT_PATH_SPLIT : 0);
     if (part & wfpt::kPassDeferred) c->path |= WFPT_PATH_FOLD;
   }
   HIP_TRY(hipGetLastError());
@@ -533,6 +546,13 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
   if (c->count || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
   const bool eng = engine_family(P, K);
   const bool lean = eng && lean_predicted(c, d);
+  if (eng && !lean && c->state) {
+    // refinement predicted: the lean pass keeps the refining chunks' level-0
+    // state, the engine's state pass completes them (and the heavy chunks)
+    if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassAll | wfpt::kPassState, d))
+      return rc;
+    return finish_sum(c, d, P, K, out, false);
+  }
   const bool fast = c->fast_only && d->no_defer;
   if (!lean && !fast) return -1;
   const int lp = lean ? wfpt::kPassLean : 0;
@@ -610,6 +630,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
   if (const char* sm = std::getenv("WFPT_SMALL")) c->small = std::strcmp(sm, "0") != 0;
+  if (const char* sm = std::getenv("WFPT_STATE")) c->state = std::strcmp(sm, "1") == 0;
   if (const char* lt = std::getenv("WFPT_LEAN_TREE")) c->lean_tree_max = std::atof(lt);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -622,8 +643,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
     e = hipHostMalloc((void**)&c->mres, 8 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->n_defer, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->n_defer, 0, 2 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
@@ -674,6 +695,7 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->fin_ticket) (void)hipFree(c->fin_ticket);
   if (c->ar) (void)hipFree(c->ar);
   c->redo.release();
+  c->st.release();
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -968,12 +990,10 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   if (c->nodes_generic) mode = -1;
   HIP_TRY(c->res.reserve(std::max<int32_t>(m, 1)));
   if (mode >= 0) {  // deferred records / listed chunks of the per-node fast path
-    if (mode == wfpt::kDirect) {
-      HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
-      HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
-    }
+    HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
+    HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>((d->n + 63) / 64, 1)));
-    HIP_TRY(hipMemsetAsync(c->n_defer, 0, sizeof(int), c->stream));
+    HIP_TRY(hipMemsetAsync(c->n_defer, 0, 2 * sizeof(int), c->stream));
   }
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
@@ -1251,7 +1271,9 @@ int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::
   st->launched = true;
   if (st->lean)
     return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d, c->ar);
-  return run_sum(c, d->x, d->n, P, K, c->ar, wfpt::kPassAll, d);
+  const int part = (st->eng && c->state && !c->count) ? wfpt::kPassAll | wfpt::kPassState
+                                                      : wfpt::kPassAll;
+  return run_sum(c, d->x, d->n, P, K, c->ar, part, d);
 }
 int ar_settle(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               const ArState& st) {

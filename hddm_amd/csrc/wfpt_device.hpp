@@ -75,6 +75,23 @@ __host__ __device__ inline int select_mode(double sz, double st, int use_adaptiv
 constexpr double kExactBelow = 1e-290;
 constexpr double kTieBand = 1e-11;
 
+// A settled density 0 < p <= kExactBelow (its tree decided with the
+// reference's operations, no near-tie flagged) when the call's outlier mixture
+// adds w_outlier p_outlier >= kMixAbsorb: any value within the fast path's
+// error of p (< 1e-289) satisfies p' (1 - p_outlier) < w_outlier p_outlier
+// 2^-54, so the reference's mixture p' (1 - p_outlier) + w_outlier p_outlier
+// (wfpt.pyx:44, :70) rounds to w_outlier p_outlier exactly and the trial's
+// output does not depend on p: it is settled as 0 (the same mixture bits)
+// instead of being recomputed on the exact path. Without the mixture
+// (full_pdf, p_outlier = 0) such a density still takes the exact path.
+constexpr double kMixAbsorb = 1e-250;
+#ifndef WFPT_TINY_MIX
+#define WFPT_TINY_MIX 1
+#endif
+__host__ __device__ inline bool tiny_absorbed(double p, double p_outlier, double w_outlier) {
+  return WFPT_TINY_MIX && p > 0.0 && p <= kExactBelow && w_outlier * p_outlier >= kMixAbsorb;
+}
+
 // UNROLL: the t-node loop fully unrolled (node positions, q hints and
 // accumulators without per-node selects or loop-carried copies; 5x the code).
 // The lean pass unrolls its boundary-uniform call site (WFPT_LEAN_UNROLL):
@@ -1110,6 +1127,13 @@ __device__ inline bool small_grid2d(const TNode& T, const ZGrid& G, double sv, d
 // stab (nullable): the grid's large-time sine table sin(k pi g_i), row k at
 // stab + 5 k (k = 1..kSinK; SinTable); null: the Chebyshev recurrence in
 // registers.
+// Returns false when a node's drift factor overflowed with a positive series
+// value (exp(c) = inf): then LITERAL fills that node with the reference's
+// literal form (below); LITERAL = false (the level-0-only passes, whose
+// register budget the rare form would take) leaves it inf. Either way the
+// caller decides: a t node's root z grid (kAdaptTZ) hands such a node's z
+// integral to a z walk, whose grids take the literal values.
+template <bool LITERAL = true>
 __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double v, double sv,
                                           double a, double (&out)[5],
                                           const double* stab = nullptr) {
@@ -1336,18 +1360,42 @@ __device__ inline bool tnode_pdf_sv_grid5(const TNode& T, const ZGrid& G, double
     clean = clean & (p[i] > 0) & !__builtin_isinf(out[i]);
   }
   if (__builtin_expect(clean, 1)) return true;
-  bool ok = true;
+  if (!LITERAL) {
+    bool ok = true;
 #pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      double r2 = out[i];
+      if (sv != 0 && p[i] < 0) r2 = __builtin_nan("");
+      if (p[i] == 0) r2 = 0.0 * T.sc;
+      ok = ok & !(__builtin_isinf(r2) && p[i] > 0);
+      out[i] = r2;
+    }
+    return ok;
+  }
+  bool ok = true;
+#pragma unroll 1
   for (int i = 0; i < 5; ++i) {
-    double r2 = out[i];
-    if (sv != 0 && p[i] < 0) r2 = __builtin_nan("");  // log(p < 0) in the reference
+    double r2 = pick5(out, i);
+    const double pi = pick5(p, i);
+    if (sv != 0 && pi < 0) r2 = __builtin_nan("");  // log(p < 0) in the reference
     // exp(log 0 + c) = 0 even if e^c = inf; 0 * sc keeps the reference's
     // 0 / (a*a) = NaN at a == 0
-    if (p[i] == 0) r2 = 0.0 * T.sc;
-    // exp(c) overflow with a finite true value: the reference's literal
-    // exp(log p + c) is the exact path's (the caller routes the trial there)
-    ok = ok & !(__builtin_isinf(r2) && p[i] > 0);
-    out[i] = r2;
+    if (pi == 0) r2 = 0.0 * T.sc;
+    // exp(c) overflow with a finite true value (sv > 0): the reference's
+    // literal form exp(log p + c) / sqrt(sv^2 x + 1) / a^2 (pdf.pxi:102), a
+    // value like the others (the stop tests keep their tie band). sv = 0: the
+    // reference's p exp(c) / a^2 (pdf.pxi:85) overflows to inf as well.
+    const bool ovf = __builtin_isinf(r2) && pi > 0;
+    ok = ok & !ovf;
+    if (ovf && sv != 0) {
+      const double w = pick5(G.g, i);
+      const double azsv = (a * w) * sv;
+      r2 = (exp(log(pi) + (((azsv * azsv) - (((2.0 * a) * v) * w)) - T.vvx) /
+                              (((2.0 * (sv * sv)) * T.xx) + 2.0)) /
+            sqrt(((sv * sv) * T.xx) + 1.0)) /
+           (a * a);
+    }
+    put5(out, i, r2);
   }
   return ok;
 }
@@ -1410,12 +1458,18 @@ __device__ inline double inner_root(const TNode& T, const ZGrid& G, double iZz, 
                                     long long& ne, bool& repair,
                                     const double* stab = nullptr) {
   double f[5];
-  if (!tnode_pdf_sv_grid5(T, G, v, sv, a, f, stab)) flags |= kFlagExact;
+  // an overflowed drift factor marks the z integral as refining: in every
+  // call sequence the t node's value then comes from a z walk, whose grids
+  // take the literal form (its values here are not used; their stop test
+  // raises no flag)
+  const bool ovf = !tnode_pdf_sv_grid5<false>(T, G, v, sv, a, f, stab);
 #pragma unroll
   for (int i = 0; i < 5; ++i) f[i] = f[i] * iZz;
   ne += 5;
   const Simp s = simp5p(G.h6, G.h12, f[0], f[1], f[2], f[3], f[4]);
-  repair = simpson_refine(s.S, s.S2, K.simps_err, K.n_sz, flags);
+  int fl = 0;
+  repair = simpson_refine(s.S, s.S2, K.simps_err, K.n_sz, fl) || ovf;
+  flags |= ovf ? 0 : fl;
   return simp_value(s);
 }
 
@@ -1458,7 +1512,10 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
     ne += 1;
     p = pdf_sv(x - t, v, sv, a, z, err, flags);
     if (flags & kFlagExact) return kExact;
-    return (p > kExactBelow || x - t <= 0) ? kFinal : kExact;
+    if (p > kExactBelow || x - t <= 0) return kFinal;
+    if (!tiny_absorbed(p, P.p_outlier, K.w_outlier)) return kExact;
+    p = 0.0;
+    return kFinal;
   }
   // adaptive families: the engine's level 0 (eng_level0, defined below) on
   // this trial's own root z grid
@@ -1555,7 +1612,13 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
 // KEEP_F = false (the lean pass, which never reads f[]): the root Simpson
 // sums are accumulated as the t nodes complete, in the reference's
 // expression order (three registers across the node loop instead of five).
-template <int MODE, bool KEEP_F = true, bool UNROLL = false>
+// Overflowed drift factors (tnode_pdf_sv_grid5): kAdaptTZ's t-node root
+// grids hand them to z walks in every pass (inner_root); kAdaptZ's root grid
+// takes the literal form when LITERAL (the engine's own level 0, not
+// unrolled), otherwise (the unrolled level-0-only passes: lean, small,
+// per-node / per-trial fast) the trial returns kTree, i.e. it is handed to the
+// engine — every call sequence gives it the same bits.
+template <int MODE, bool KEEP_F = true, bool UNROLL = false, bool LITERAL = !UNROLL>
 __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs& K,
                                    const ZGrid& G, double& p, double (&f)[5], long long& ne,
                                    unsigned& pend, const double* stab = nullptr) {
@@ -1571,7 +1634,9 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
     const double iw = 1.0 / (ub - lb);
     const TNode T = tnode_setup(tr.x - P.t, tr.v, P.sv, P.a, K.err);
     if (T.amb) return kExact;
-    if (!tnode_pdf_sv_grid5(T, G, tr.v, P.sv, P.a, f, stab)) return kExact;
+    // (kAdaptZ: the root grid's values are the tree's; an overflow hands a
+    // level-0-only pass's trial to the engine, which uses the literal values)
+    if (!tnode_pdf_sv_grid5<LITERAL>(T, G, tr.v, P.sv, P.a, f, stab) && !LITERAL) return kTree;
 #pragma unroll
     for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
     ne += 5;
@@ -1585,7 +1650,7 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
 #define WFPT_L0_ACC_NODE(j)                                                      \
   {                                                                              \
     bool pj;                                                                     \
-    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab); \
+    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);  \
     if (flags & kFlagExact) return kExact;                                       \
     if (pj) pend |= 1u << ((j) * (kTreeW / 4));                                  \
     const double x4 = X + (4 * y);                                               \
@@ -1613,12 +1678,15 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
       if (flags & kFlagExact) return kExact;
       if (refine) return kTree;
       p = s.S2 + (s.S2 - s.S) / 15;
-      return (p > kExactBelow || structural) ? kFinal : kExact;
+      if (p > kExactBelow || structural) return kFinal;
+      if (!tiny_absorbed(p, P.p_outlier, K.w_outlier)) return kExact;
+      p = 0.0;
+      return kFinal;
     }
 #define WFPT_L0_F_NODE(j)                                                        \
   {                                                                              \
     bool pj;                                                                     \
-    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab); \
+    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);  \
     if (flags & kFlagExact) return kExact;                                       \
     if (pj) pend |= 1u << ((j) * (kTreeW / 4));                                  \
     if ((j) == 0) f[0] = y;                                                      \
@@ -1643,7 +1711,10 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
   if (flags & kFlagExact) return kExact;
   if (refine) return kTree;
   p = s.S2 + (s.S2 - s.S) / 15;
-  return (p > kExactBelow || structural) ? kFinal : kExact;
+  if (p > kExactBelow || structural) return kFinal;
+  if (!tiny_absorbed(p, P.p_outlier, K.w_outlier)) return kExact;
+  p = 0.0;
+  return kFinal;
 }
 template <int MODE, bool UNROLL>
 __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,

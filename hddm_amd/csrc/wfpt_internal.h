@@ -31,7 +31,17 @@ struct Work {
   unsigned char* redo;        // [chunks]
   int* tree_any;              // device word: some chunk of the call refined (0 at rest)
   int64_t nslots;
+  // State handoff (kPassState): the lean pass keeps level 0's values and
+  // writes each refining chunk's level-0 state here (kStateWords x 64 per
+  // chunk, word-major), which the engine's state pass reads instead of
+  // recomputing level 0. Null outside that sequence.
+  double* st;                 // [chunks * 64 * kStateWords]
+  const unsigned char* pred;  // [chunks] the call's heavy chunks (the engine splits them), or null
+  unsigned char* next_pred;   // [chunks] the record for the next call (the lean pass writes 0)
 };
+// level-0 state of a lane: f at the root t interval's 5 nodes, p, and
+// oc | pend << 2 | evaluations << 24 as an integer in a double's bits
+constexpr int kStateWords = 7;
 
 constexpr int kPhaseWaves = 16384;
 
@@ -81,7 +91,12 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 // and counted as deferred), and kPassRedo runs the engine over the flagged
 // chunks (before the fold). fast_done (optional) is recorded right after the
 // level-0 / trial kernel.
-constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPassRedo = 8;
+// kPassState (adaptive engine families, with kPassAll): the lean pass keeps
+// level 0's state for the refining chunks (Work::st) and the engine's state
+// pass completes them (plus the dataset's split heavy chunks) without
+// recomputing level 0.
+constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPassRedo = 8,
+              kPassState = 16;
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,
@@ -115,9 +130,11 @@ void launch_publish(const double* res, double* out, unsigned long long seq, hipS
 // (one thread, stream order: the all-reduce of a rank whose local pass failed)
 void launch_poison(double* res, hipStream_t s);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
-// two-pass fast path; *n_defer must be 0 on the stream: the direct family's
-// deferred (index, row) records in d_idx / d_par (up to n), the adaptive
-// families' listed chunks in clist (up to (n + 63) / 64)), or -1 (mixed /
+// two-pass fast path; n_defer[0..1] must be 0 on the stream: the direct
+// family's deferred (index, row) records in d_idx / d_par (up to n) counted in
+// n_defer[0]; the adaptive families' listed chunks in clist (up to
+// (n + 63) / 64) counted in n_defer[0] and the records their chunk engine
+// hands on in d_idx / d_par counted in n_defer[1]), or -1 (mixed /
 // fixed Simpson: one generic per-trial kernel with a per-lane mode). prof
 // (COUNT builds, evals != null): the node tallies of wfpt_profile_lists.
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,

@@ -417,6 +417,7 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
     on = on && !(cl.fl[owner] & kFlagStop);
     double y[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     int flip = 0;
+    bool ovf = false;  // a drift factor overflowed (tnode_pdf_sv_grid5)
     if (on) {
       const double xo = cl.X[owner];
       flip = xo > 0;
@@ -437,8 +438,8 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
       const TNode T = tnode_setup_r(xx, vo, sv, a, ia2, err, qh, known, kd);
       if (T.amb) atomicOr(&cl.fl[owner], (int)kFlagExact);
       if (MODE == kAdaptT) y[0] = tnode_pdf_sv(T, flip ? 1. - z : z, vo, sv, a);
-      else if (!tnode_pdf_sv_grid5(T, cl.tab.G[flip][gs], vo, sv, a, y))
-        atomicOr(&cl.fl[owner], (int)kFlagExact);  // exp(c) overflow: the exact path
+      else
+        ovf = !tnode_pdf_sv_grid5(T, cl.tab.G[flip][gs], vo, sv, a, y);  // literal values
     }
     if (stage == 0) {
       bool pend = false;
@@ -461,7 +462,9 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
           const Simp s = simp5p(gr.h6, gr.h12, y[0] * izf, y[1] * izf, y[2] * izf, y[3] * izf,
                                 y[4] * izf);
           int f = 0;
-          pend = simpson_refine(s.S, s.S2, se, nsz, f);
+          // an overflowed root grid: the z walk (inner_root's rule)
+          pend = simpson_refine(s.S, s.S2, se, nsz, f) || ovf;
+          if (ovf) f = 0;
           if (f) atomicOr(&cl.fl[owner], f);
           else if (!pend) cl.F[pos * 64 + owner] = simp_value(s) * iwt;
           if (COUNT) atomicAdd(&cl.cnt[owner], 5);
@@ -525,6 +528,10 @@ __device__ inline void tree_density(const TrialArgs& A, const ChunkLds<TW>& cl, 
   // structural zero: no evaluation point with x - t_node > 0
   const bool structural = (MODE == kAdaptZ) ? tr.x - A.P.t <= 0 : tr.x - P[0] <= 0;
   defer = (fl & kFlagExact) || need || !(p > kExactBelow || structural);
+  if (defer && !(fl & kFlagExact) && !need && tiny_absorbed(p, A.P.p_outlier, A.K.w_outlier)) {
+    defer = false;  // the mixture absorbs it (tiny_absorbed)
+    p = 0.0;
+  }
   rf = kFlagExact;
 }
 
@@ -628,10 +635,15 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
     record_heavy(S, c, znc > kHeavyZ);
     S.done[slot] = 0;
     S.zn[slot] = 0;
+    if (W.redo) W.redo[c] = 0;  // state pass: the lean pass flagged the split chunk
   }
 }
 
-template <int MODE, bool COUNT, int OUT>
+// STATE (kPassState): the chunks' level 0 comes from the lean pass
+// (W.st: f, p, outcome, pending z integrals) instead of being recomputed; the
+// kernel carries no level-0 code. Only the chunks the lean pass flagged in
+// W.redo (refining, or split) run.
+template <int MODE, bool COUNT, int OUT, bool STATE = false>
 __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work W, EngTables tab,
                                                               Split S) {
   __shared__ ChunkLds<1> lds[kEngWaves];
@@ -663,7 +675,16 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
     // ---- level 0, each lane its own trial, in registers ----
     double f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     unsigned pend0 = 0u;
-    if (own) {
+    if (STATE) {  // the lean pass's level 0 of this chunk (kStateWords words)
+      const double* st = W.st + c * (64 * kStateWords);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) f0[k] = st[k * 64 + lane];
+      p = st[5 * 64 + lane];
+      const long long w = __double_as_longlong(st[6 * 64 + lane]);
+      oc = own ? (int)(w & 3) : kFinal;
+      pend0 = (unsigned)((w >> 2) & 0x3fffff);
+      ne0 = w >> 24;
+    } else if (own) {
       const ZGrid G = cl.tab.G[x0 > 0][kGridRoot];
       oc = eng_level0<MODE>(x0, A.P, A.K, G, p, f0, ne0, pend0);
     }
@@ -783,7 +804,13 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 #define WFPT_SIN_TABLE 1
 #endif
 
-template <int MODE, bool COUNT, int OUT>
+// STATE (kPassState, the sequence predicted for data that refines): level 0
+// keeps its node values (KEEP_F) and a refining chunk leaves its lanes'
+// level-0 state in W.st for the engine's state pass instead of nothing; the
+// dataset's heavy chunks (W.pred, split by the engine) are skipped; every
+// chunk's next-call split record starts at 0 (the engine records the heavy
+// ones).
+template <int MODE, bool COUNT, int OUT, bool STATE = false>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
 #if WFPT_LEAN_REVERSE
@@ -795,9 +822,19 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
   if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
+  if (STATE) {
+    if (lane == 0 && W.next_pred) W.next_pred[c] = 0;
+    if (W.pred && W.pred[c]) {  // split by the engine's state pass
+      if (lane == 0) {
+        W.redo[c] = 1;
+        if (sum_out(OUT)) A.zeros[c] = kZeroDefer;
+      }
+      return;
+    }
+  }
   const bool own = i < A.n;
   const double x0 = own ? A.x[i] : 0.0;
-  double p = 0.0, f0[5];
+  double p = 0.0, f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
   long long ne0 = 0;
   unsigned pend0 = 0u;
   int oc = kFinal;
@@ -811,15 +848,23 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
   const int b = (bp == bo) ? 1 : 0;  // every trial upper: 1; otherwise lower first
   if (own && pos == (b != 0))
-    oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
+    oc = eng_level0_t<MODE, STATE, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
                                    zgrid_uniform(R, b), p, f0, ne0, pend0,
                                    WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
   if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
     if (own && pos)
-      oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
+      oc = eng_level0_t<MODE, STATE, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
                                      ne0, pend0, WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
   }
   if (__ballot(oc == kTree) != 0ull) {
+    if (STATE) {
+      double* st = W.st + c * (64 * kStateWords);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) st[k * 64 + lane] = f0[k];
+      st[5 * 64 + lane] = p;
+      st[6 * 64 + lane] = __longlong_as_double((long long)oc | ((long long)pend0 << 2) |
+                                               ((long long)ne0 << 24));
+    }
     if (lane == 0) {
       W.redo[c] = 1;
       // finalize reports the call as deferred: the host runs the redo pass
@@ -1461,17 +1506,21 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
 // fast pass), so a chunk's terms do not depend on which lanes deferred.
 // Replaces one wave per deferred trial: a call where most trials refine (an
 // MCMC proposal far in the tails) runs 64 trials per wave.
+// Trials the rounds hand on (the exact path, trees deeper than kTreeDepth)
+// become (2 i + exact, parameter row) records for node_defer_kernel (one lane
+// each), so this kernel carries neither path's registers nor stack.
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
-    const int* clist, const int* n_chunks, unsigned long long* evals, int* status, int* prof) {
+    const int* clist, const int* n_chunks, int64_t* d_rec, Params* d_par, int* n_rec,
+    unsigned long long* evals, int* prof) {
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
   const int nc = *n_chunks;
   const int nwaves = (int)gridDim.x * kEngWaves;
   long long ne = 0;
-  int errf = 0, nseg = 0, nex = 0, nwk = 0;
+  int nseg = 0, nex = 0, nwk = 0;
   Tally ty;
   for (int k = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
        k < nc; k += nwaves) {
@@ -1538,20 +1587,25 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
         tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
         if (COUNT) n1 = cl.cnt[lane];
       }
-      if (defer) {
-        n1 = 0;
-        if (COUNT) ++((rf & kFlagExact) ? nex : nwk);
-        p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
-                              : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+      const unsigned long long db = __ballot(defer);
+      if (db) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(n_rec, __popcll(db));
+        base = __shfl(base, 0, 64);
+        if (defer) {
+          const int r = base + __popcll(db & lanemask_lt(lane));
+          d_rec[r] = 2 * i + ((rf & kFlagExact) ? 1 : 0);
+          d_par[r] = Q;
+          if (COUNT) ++((rf & kFlagExact) ? nex : nwk);
+        }
       }
-      if (mine) {
+      if (mine && !defer) {
         ne += n1;
         lp[i] = node_logp(p, Q, K);
       }
       wave_sync();  // the next segment rebuilds this wave's LDS
     }
   }
-  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
   if (COUNT) {
     ne = wave_sum_ll(ne);
     nex = (int)wave_sum_ll(nex);
@@ -1569,6 +1623,31 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
       atomicAdd(&prof[9], ty.z[1]);
       atomicAdd(&prof[10], ty.z[2]);
     }
+  }
+}
+
+// The records node_chunk_kernel handed on, one lane each: the exact path or
+// the per-lane walk (fold_kernel's operations), then the node's term.
+template <int MODE, bool COUNT>
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_defer_kernel(
+    const double* x, Knobs K, double* lp, const int64_t* d_rec, const Params* d_par,
+    const int* n_rec, unsigned long long* evals, int* status) {
+  const int nd = *n_rec;
+  long long ne = 0;
+  int errf = 0;
+  for (int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x; k < nd; k += (int64_t)gridDim.x * 64) {
+    const int64_t r = d_rec[k], i = r >> 1;
+    const Params Q = d_par[k];
+    long long n1 = 0;
+    const double p = (r & 1) ? exact_pdf(x[i], Q, K, &n1, &errf)
+                             : fallback_pdf<MODE>(x[i], Q, K, &n1, &errf);
+    ne += n1;
+    lp[i] = node_logp(p, Q, K);
+  }
+  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
+  if (COUNT) {
+    ne = wave_sum_ll(ne);
+    if (threadIdx.x == 0) atomicAdd(evals, (unsigned long long)ne);
   }
 }
 
@@ -1747,15 +1826,30 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
   return A;
 }
 
+// the state sequence's kernels exist for the summing outputs without counting
+template <bool COUNT, int OUT>
+constexpr bool kHasState = !COUNT && sum_out(OUT);
+
 template <int MODE, bool COUNT, int OUT>
 static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
-                     bool lean, hipStream_t s, hipEvent_t fast_done) {
+                     bool lean, bool state, hipStream_t s, hipEvent_t fast_done) {
   if constexpr (MODE == kDirect) {
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W);
-  } else if (lean) {
+  } else if (lean || state) {
     RootGrids R;
     root_grids(A.P, R);
+    if constexpr (kHasState<COUNT, OUT>) {
+      if (state) {
+        Work Ws = W;
+        Ws.pred = S.n > 0 ? S.pred : nullptr;
+        Ws.next_pred = S.next_pred;
+        hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT, true>), dim3(fast_blocks(A.n)),
+                           dim3(kFastBlock), 0, s, A, Ws, R);
+        if (fast_done) (void)hipEventRecord(fast_done, s);
+        return;
+      }
+    }
     hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W, R);
   } else {
@@ -1768,10 +1862,19 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
 }
 
 template <int MODE, bool COUNT, int OUT>
-static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, bool redo,
-                         hipStream_t s) {
+static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
+                         bool redo, bool state, hipStream_t s) {
   const int64_t nw = (A.n + 63) / 64;
   if constexpr (MODE != kDirect) {
+    if constexpr (kHasState<COUNT, OUT>) {
+      if (state) {  // the flagged chunks from their lean-pass state, the split units first
+        const int64_t units = (int64_t)S.n * kSplit + nw;
+        hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT, true>),
+                           dim3((units + kEngWaves - 1) / kEngWaves), dim3(kEngBlock), 0, s, A, W,
+                           T, S);
+        redo = false;
+      }
+    }
     if (redo)  // the engine over the chunks the lean pass flagged (one wave each)
       hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>), dim3((nw + kEngWaves - 1) / kEngWaves),
                          dim3(kEngBlock), 0, s, A, W, T, Split{});
@@ -1786,19 +1889,22 @@ static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, c
                         hipStream_t s, hipEvent_t fast_done) {
   // the engine's tables (the lean pass alone needs only its root grids)
   EngTables T;
-  const bool engine = ((part & kPassFast) && !(part & kPassLean)) || (part & kPassRedo);
+  const bool state = (part & kPassState) != 0 && W.st != nullptr;
+  const bool engine =
+      ((part & kPassFast) && !(part & kPassLean)) || (part & kPassRedo) || state;
   if (mode >= kAdaptT && mode <= kAdaptTZ && engine) eng_tables(A.P, T);
-  // W.redo is live only in the lean and redo passes (a full engine launch
-  // processes every chunk); the host never combines kPassRedo with a full
-  // engine level-0 pass
+  // W.redo is live only in the lean, redo and state passes (a full engine
+  // launch processes every chunk); the host never combines kPassRedo with a
+  // full engine level-0 pass
   Work F = W;
-  F.redo = (part & (kPassLean | kPassRedo)) ? W.redo : nullptr;
-#define FAST_AND_DEFERRED(M_)                                               \
-  do {                                                                      \
-    if (part & kPassFast)                                                   \
-      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, s, fast_done); \
-    if (part & kPassDeferred)                                               \
-      run_deferred<M_, COUNT, OUT>(A, F, T, (part & kPassRedo) != 0, s);    \
+  F.redo = (part & (kPassLean | kPassRedo)) || state ? W.redo : nullptr;
+  if (!state) F.st = nullptr;
+#define FAST_AND_DEFERRED(M_)                                                       \
+  do {                                                                              \
+    if (part & kPassFast)                                                           \
+      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, state, s, fast_done); \
+    if (part & kPassDeferred)                                                       \
+      run_deferred<M_, COUNT, OUT>(A, F, T, S, (part & kPassRedo) != 0, state, s);  \
   } while (0)
   switch (mode) {
     case kDirect: FAST_AND_DEFERRED(kDirect); break;
@@ -1922,7 +2028,10 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     const int64_t nw = (n + 63) / 64;
     const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
-                       n, P, K, lp, clist, n_defer, evals, status, prof);
+                       n, P, K, lp, clist, n_defer, d_idx, d_par, n_defer + 1, evals, prof);
+    const int64_t g = std::min<int64_t>(nw, 2048);
+    hipLaunchKernelGGL((node_defer_kernel<MODE, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp, d_idx,
+                       d_par, n_defer + 1, evals, status);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;

@@ -338,5 +338,6 @@ def test_two_rank_gloo_with_device_triples(gpu, oracle_lib):
             assert abs(got[r] - ref) <= 1e-11 * math.fsum(np.abs(terms)), (r, got[r], ref)
     x0 = x.copy()
     x0[-5] = 0.05  # below t - st/2 on rank 1: -inf everywhere
-    res0 = _run(x0, None, kn, None, worker=_device_worker, extra=[calm])
+    kn0 = kn[:5] + (0.0, 0.1)  # p_outlier 0: a zero Wiener density is a zero mixture density
+    res0 = _run(x0, None, kn0, None, worker=_device_worker, extra=[calm])
     assert all(g[0] == -math.inf for g in res0)

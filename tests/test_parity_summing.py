@@ -85,7 +85,7 @@ def path_names(bits):
     from hddm_amd import _lib
     names = {_lib.PATH_LEAN: "lean", _lib.PATH_ENGINE: "engine", _lib.PATH_SMALL: "small",
              _lib.PATH_REDO: "redo", _lib.PATH_FOLD: "fold", _lib.PATH_DIRECT: "direct",
-             _lib.PATH_FIXED: "fixed", _lib.PATH_SPLIT: "split"}
+             _lib.PATH_FIXED: "fixed", _lib.PATH_SPLIT: "split", _lib.PATH_STATE: "state"}
     return {v for k, v in names.items() if bits & k}
 
 
@@ -116,8 +116,8 @@ def test_lean_kernel_per_trial_on_bench_dataset(gpu, oracle_lib):
     x = gpu.gen_rts_from_cdf(*PINNED, samples=1_000_000, dt=1e-3)
     ref = ref_terms(oracle_lib, x, PINNED)
     ds = gpu.Dataset(x)
-    first = ds.wiener_like(*PINNED, *KN)  # full sequence: the engine
-    assert "engine" in path_names(ctx.last_path())
+    first = ds.wiener_like(*PINNED, *KN)  # nothing predicted yet: the state sequence
+    assert path_names(ctx.last_path()) & {"engine", "state"}, path_names(ctx.last_path())
     tot, terms, path = summing_vs_trials(ctx, ds, PINNED)
     assert path_names(path) == {"lean"}, path_names(path)
     assert tot == first
@@ -161,48 +161,73 @@ def test_stress_sets_per_trial_engine_and_lean(gpu, oracle_lib, monkeypatch, k):
     ctx_l.close()
 
 
+@pytest.fixture(scope="module")
+def lean_ctx(gpu):
+    """A second context whose resident calls always take the lean level-0
+    pass (WFPT_LEAN_TREE=1: chunks that refine go to the engine's redo pass),
+    so the lean / small kernels run on data that would otherwise predict the
+    engine."""
+    from hddm_amd import _lib
+    old = os.environ.get("WFPT_LEAN_TREE")
+    os.environ["WFPT_LEAN_TREE"] = "1.0"
+    try:
+        ctx = _lib.Context(0)
+    finally:
+        if old is None:
+            del os.environ["WFPT_LEAN_TREE"]
+        else:
+            os.environ["WFPT_LEAN_TREE"] = old
+    yield ctx
+    ctx.close()
+
+
+def _both_contexts(gpu, lean_ctx, x, args, what, oracle_lib, need):
+    """Per trial and per chunk on the default context's predicted path and on
+    the forced-lean one (which must include a kernel of `need`); the two
+    totals are bitwise equal."""
+    from hddm_amd import _lib
+    ref = ref_terms(oracle_lib, x, args)
+    tots = []
+    for ctx in (_lib.context(), lean_ctx):
+        ds = gpu.Dataset(x, ctx=ctx)
+        ds.wiener_like(*args, *KN)
+        tot, terms, path = summing_vs_trials(ctx, ds, args)
+        if ctx is lean_ctx:
+            assert path_names(path) & need, (what, path_names(path))
+        assert_terms(terms, ref, f"{what} {path_names(path)}")
+        assert_chunks(ctx, ds, ref, f"{what} {path_names(path)}")
+        tots.append(tot)
+        ds.close()
+    assert tots[0] == tots[1], (what, tots)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n_lower,n", [(37, 1000), (100, 3000), (64, 200), (1, 130)])
-def test_mixed_boundary_wave_per_trial(gpu, oracle_lib, n_lower, n):
+def test_mixed_boundary_wave_per_trial(gpu, oracle_lib, lean_ctx, n_lower, n):
     """The wave where the dataset's boundary-ordered trials switch from the
     lower to the upper boundary runs the lean level 0 at two call sites (the
     scalar root grid of each boundary): per trial and per chunk, for the
     2-D, 1-D (t, z) families."""
-    from hddm_amd import _lib
-    ctx = _lib.context()
     rng = np.random.default_rng(n_lower * 7 + n)
     mag = 0.33 + rng.gamma(2.0, 0.35, n)
     x = np.where(np.arange(n) < n_lower, -mag, mag)
     rng.shuffle(x)
     for args in (PINNED, ST_ONLY, SZ_ONLY):
-        ref = ref_terms(oracle_lib, x, args)
-        ds = gpu.Dataset(x)
-        ds.wiener_like(*args, *KN)
-        tot, terms, path = summing_vs_trials(ctx, ds, args)
-        assert path_names(path) & {"lean", "small"}, path_names(path)
-        assert_terms(terms, ref, f"mixed wave {args}")
-        assert_chunks(ctx, ds, ref, f"mixed wave {args}")
+        _both_contexts(gpu, lean_ctx, x, args, f"mixed wave {n_lower}/{n} {args}", oracle_lib,
+                       {"lean", "small"})
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [1, 17, 63, 64, 65, 128, 200, 250, 256])
-def test_node_sized_one_launch_per_trial(gpu, oracle_lib, n):
+def test_node_sized_one_launch_per_trial(gpu, oracle_lib, lean_ctx, n):
     """Datasets of <= 256 trials (one HDDM node: what the install()ed
-    wfpt_like runs per node per logp) take small_kernel once predicted:
-    per trial and per chunk against the reference, every family."""
-    from hddm_amd import _lib
-    ctx = _lib.context()
+    wfpt_like runs per node per logp) take small_kernel once the lean pass is
+    predicted: per trial and per chunk against the reference, every family."""
     rng = np.random.default_rng(1000 + n)
     x = rng.choice([-1.0, 1.0], n) * (0.32 + rng.gamma(2.0, 0.4, n))
     for args in (SIMPLE, PINNED, ST_ONLY, SZ_ONLY):
-        ref = ref_terms(oracle_lib, x, args)
-        ds = gpu.Dataset(x)
-        first = ds.wiener_like(*args, *KN)
-        tot, terms, path = summing_vs_trials(ctx, ds, args)
-        assert "small" in path_names(path), (n, args, path_names(path))
-        assert tot == first
-        assert_terms(terms, ref, f"node-sized {n} {args}")
-        assert_chunks(ctx, ds, ref, f"node-sized {n} {args}")
+        _both_contexts(gpu, lean_ctx, x, args, f"node-sized {n} {args}", oracle_lib,
+                       {"small"})
 
 
 def _seed3():

@@ -11,3 +11,11 @@ timeout -k 10 180 python -u tools/slow_node_probe.py tools/scratch/slow_seed3.np
 tail -2 gpurun_out/r04/slow_probe.log
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 3 --cpu-seconds 5 > gpurun_out/r04/bench.log 2>&1 || { echo "BENCH_FAIL rc=$?"; exit 1; }
 tail -1 gpurun_out/r04/bench.log
+if [ -n "${STRESS:-}" ]; then
+  timeout -k 10 300 python -u tools/stress_probe.py --reps 10 --json gpurun_out/r04/stress.json > gpurun_out/r04/stress.log 2>&1 || { echo "STRESS_FAIL rc=$?"; exit 1; }
+  tail -6 gpurun_out/r04/stress.log
+fi
+if [ -n "${STRESS_AB:-}" ]; then
+  WFPT_STATE=0 timeout -k 10 300 python -u tools/stress_probe.py --reps 10 --json gpurun_out/r04/stress_nostate.json > gpurun_out/r04/stress_nostate.log 2>&1 || { echo "STRESS0_FAIL rc=$?"; exit 1; }
+  tail -6 gpurun_out/r04/stress_nostate.log
+fi
