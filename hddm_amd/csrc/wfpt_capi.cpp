@@ -138,7 +138,10 @@ struct wfpt_ctx {
   DevBuf<int> wl_n;          // per chunk: deferred trials
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
   DevBuf<unsigned char> redo;  // per chunk: the lean pass left it to the engine (0 at rest)
-  DevBuf<double> st;         // per chunk: level-0 state of the state sequence (kPassState)
+  DevBuf<double> st;         // records sequence (kPassState): level-0 state per record
+  DevBuf<int> rec;           // ... and each record's slot
+  DevBuf<double> dens;       // per slot: densities of deferred trials
+  int* nrec = nullptr;       // device: records of the call (0 at rest)
   int* tree_any = nullptr;   // device: some chunk refined in-wave (finalize reports + clears)
   double* fin = nullptr;     // device: multi-block finalize scratch (3 x 64 doubles)
   int* fin_ticket = nullptr; // device: its last-block ticket (0 at rest)
@@ -162,7 +165,7 @@ struct wfpt_ctx {
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
   bool small = true;           // WFPT_SMALL=0: one-block calls keep the separate finalize
-  bool state = false;          // WFPT_STATE=1: refining calls hand level 0 from the lean pass to the engine
+  bool state = false;          // WFPT_STATE=1: refining calls run the records sequence, not the chunk engine
   // WFPT_LEAN_TREE: the largest fraction of refining chunks (last call) for
   // which the lean pass + engine redo of those chunks beats the engine over
   // every chunk
@@ -179,6 +182,9 @@ struct wfpt_ctx {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  // the context's live datasets: wfpt_close releases their device memory and
+  // detaches them (a dataset destroyed after its context only frees itself)
+  std::vector<wfpt_ds*> dsets;
 };
 
 constexpr int64_t kSplitCap = 8192;  // heavy chunks a dataset records per call
@@ -225,6 +231,9 @@ struct DeviceGuard {
   explicit DeviceGuard(int dev) {
     (void)hipGetDevice(&prev);
     if (prev != dev) (void)hipSetDevice(dev);
+    // a stale error of an earlier, already reported runtime call must not be
+    // read as this call's launch failure (hipGetLastError after launches)
+    (void)hipGetLastError();
   }
   ~DeviceGuard() {
     int cur = -1;
@@ -232,6 +241,8 @@ struct DeviceGuard {
     if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+void ds_free_device(wfpt_ds* d);  // defined with wfpt_dataset_destroy
 
 wfpt::Params to_params(const wfpt_params* p) {
   wfpt::Params q;
@@ -286,6 +297,7 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   HIP_TRY(c->wl.reserve(ns));
   HIP_TRY(c->wl_n.reserve(nw));
   HIP_TRY(c->rflag.reserve(ns));
+  HIP_TRY(c->dens.reserve(ns));
   if (c->redo.cap < (size_t)nw) {
     HIP_TRY(c->redo.reserve(nw));
     HIP_TRY(hipMemsetAsync(c->redo.p, 0, c->redo.cap, c->stream));
@@ -298,9 +310,10 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   W->prof = c->prof;
   W->phase = c->phase;
   W->nslots = ns;
+  W->dens = c->dens.p;
   W->st = nullptr;
-  W->pred = nullptr;
-  W->next_pred = nullptr;
+  W->rec = nullptr;
+  W->nrec = c->nrec;
   return WFPT_OK;
 }
 
@@ -380,8 +393,14 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   if (int rc = reserve_work(c, n, &W)) return rc;
   const bool adaptive = wfpt::has_deferred_pass(P, K);
   if ((part & wfpt::kPassState) && engine_family(P, K)) {
-    HIP_TRY(c->st.reserve((size_t)((n + 63) / 64) * 64 * wfpt::kStateWords));
+    const size_t ns = (size_t)((n + 63) / 64) * 64;
+    HIP_TRY(c->st.reserve(ns * wfpt::kStateWords));
+    HIP_TRY(c->rec.reserve(ns));
     W.st = c->st.p;
+    W.rec = c->rec.p;
+    // 0 at rest (fold_kernel resets it); cleared here too so that a sequence
+    // cut short by an error cannot leave stale records for the next one
+    if (part & wfpt::kPassFast) HIP_TRY(hipMemsetAsync(c->nrec, 0, sizeof(int), c->stream));
   } else {
     part &= ~wfpt::kPassState;
   }
@@ -395,7 +414,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   // heavy-chunk splitting belongs to full engine calls (not the lean / redo
   // passes)
   const bool eng = d && d->hcount && engine_family(P, K) &&
-                   !(part & (wfpt::kPassLean | wfpt::kPassRedo));
+                   !(part & (wfpt::kPassLean | wfpt::kPassRedo | wfpt::kPassState));
   // one block of trials, level-0 pass only (direct family, or the lean pass):
   // level 0 and finalize in one launch (WFPT_SMALL=0: two launches)
   const bool level0_only = adaptive && (engine_family(P, K)
@@ -422,8 +441,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
                               ? WFPT_PATH_LEAN
                               : (WFPT_PATH_ENGINE | (S.n > 0 ? WFPT_PATH_SPLIT : 0));
     if (!direct && (part & wfpt::kPassRedo)) c->path |= WFPT_PATH_REDO;
-    if (part & wfpt::kPassState)
-      c->path |= WFPT_PATH_STATE | ((part & wfpt::kPassDeferred) && S.n > 0 ? WFPT_PATH_SPLIT : 0);
+    if (part & wfpt::kPassState) c->path |= WFPT_PATH_STATE;
     if (part & wfpt::kPassDeferred) c->path |= WFPT_PATH_FOLD;
   }
   HIP_TRY(hipGetLastError());
@@ -551,7 +569,7 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
     // state, the engine's state pass completes them (and the heavy chunks)
     if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassAll | wfpt::kPassState, d))
       return rc;
-    return finish_sum(c, d, P, K, out, false);
+    return finish_sum(c, d, P, K, out, true);  // no engine pass: no heavy-chunk record
   }
   const bool fast = c->fast_only && d->no_defer;
   if (!lean && !fast) return -1;
@@ -648,6 +666,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->nrec, sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->nrec, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->ar, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMemset(c->ar, 0, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin_ticket, sizeof(int));
@@ -671,6 +691,11 @@ void wfpt_close(wfpt_ctx* c) {
   if (!c) return;
   DeviceGuard g(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (wfpt_ds* d : c->dsets) {  // detached: destroying one later frees only its host part
+    ds_free_device(d);
+    d->ctx = nullptr;
+  }
+  c->dsets.clear();
   if (c->comm) (void)ncclCommDestroy(c->comm);
   c->x.release();
   c->part.release();
@@ -696,6 +721,9 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->ar) (void)hipFree(c->ar);
   c->redo.release();
   c->st.release();
+  c->rec.release();
+  c->dens.release();
+  if (c->nrec) (void)hipFree(c->nrec);
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -804,16 +832,17 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
   if (e == hipSuccess) e = hipMalloc((void**)&d->hzn, d->split_cap * sizeof(int));
   if (e == hipSuccess) e = hipMemset(d->hzn, 0, d->split_cap * sizeof(int));
   if (e != hipSuccess) {
-    wfpt_dataset_destroy(d);
+    ds_free_device(d);
+    delete d;
     return fail(WFPT_ERR_HIP, std::string("wfpt_dataset_create: ") + hipGetErrorString(e));
   }
+  c->dsets.push_back(d);
   *out = d;
   return WFPT_OK;
 }
 
-void wfpt_dataset_destroy(wfpt_ds* d) {
-  if (!d) return;
-  DeviceGuard g(d->ctx ? d->ctx->device : 0);
+namespace {
+void ds_free_device(wfpt_ds* d) {
   if (d->x) (void)hipFree(d->x);
   if (d->node) (void)hipFree(d->node);
   if (d->off) (void)hipFree(d->off);
@@ -826,6 +855,28 @@ void wfpt_dataset_destroy(wfpt_ds* d) {
   if (d->hmeta) (void)hipFree(d->hmeta);
   if (d->hdone) (void)hipFree(d->hdone);
   if (d->hzn) (void)hipFree(d->hzn);
+  d->x = nullptr;
+  d->node = nullptr;
+  d->off = nullptr;
+  d->hpred[0] = d->hpred[1] = nullptr;
+  d->hlist[0] = d->hlist[1] = nullptr;
+  d->hcount = nullptr;
+  d->hlp = nullptr;
+  d->hmeta = nullptr;
+  d->hdone = nullptr;
+  d->hzn = nullptr;
+}
+}  // namespace
+
+void wfpt_dataset_destroy(wfpt_ds* d) {
+  if (!d) return;
+  if (wfpt_ctx* c = d->ctx) {
+    std::lock_guard<std::mutex> lk(c->mu);
+    DeviceGuard g(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->dsets.erase(std::remove(c->dsets.begin(), c->dsets.end(), d), c->dsets.end());
+    ds_free_device(d);
+  }
   delete d;
 }
 
@@ -1262,7 +1313,7 @@ namespace {
 // launch would dispatch one wave per chunk: ~48k blocks at 12.5M trials).
 // After ar_settle, c->ar holds the rank's triple in stream order.
 struct ArState {
-  bool eng = false, lean = false, launched = false;
+  bool eng = false, lean = false, state = false, launched = false;
 };
 int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               ArState* st) {
@@ -1271,9 +1322,9 @@ int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::
   st->launched = true;
   if (st->lean)
     return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d, c->ar);
-  const int part = (st->eng && c->state && !c->count) ? wfpt::kPassAll | wfpt::kPassState
-                                                      : wfpt::kPassAll;
-  return run_sum(c, d->x, d->n, P, K, c->ar, part, d);
+  st->state = st->eng && c->state && !c->count;
+  return run_sum(c, d->x, d->n, P, K, c->ar,
+                 st->state ? wfpt::kPassAll | wfpt::kPassState : wfpt::kPassAll, d);
 }
 int ar_settle(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               const ArState& st) {
@@ -1290,7 +1341,7 @@ int ar_finish(wfpt_ctx* c, const wfpt_ds* d, const ArState& st, double* out) {
   wfpt::launch_publish(c->ar, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
-  split_advance(d, st.eng && !st.lean, c->mres);
+  split_advance(d, st.eng && !st.lean && !st.state, c->mres);
   const int rc = decode_sum(c, c->mres, out);
   if (rc == WFPT_OK && st.eng) note_tree(d, c->mres);
   return rc;
@@ -1404,7 +1455,7 @@ int wfpt_wiener_like_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
   double h[8];
   HIP_TRY(hipMemcpyAsync(h, c->ar, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  split_advance(d, st.eng && !st.lean, h);
+  split_advance(d, st.eng && !st.lean && !st.state, h);
   if (st.eng) note_tree(d, h);
   d->no_defer = false;
   (void)finish_profile(c);

@@ -110,6 +110,8 @@ enum Flag : int {
   kFlagBudget = 2,    // more than kEvalBudget pdf_sv evaluations in one trial
   kFlagExact = 4,     // recompute on the exact path
   kFlagFallback = 8,  // tree deeper than the breadth-first levels: per-lane walk
+  kFlagRefined = 32,  // (engine rounds) the owner refined at level 0: root test or a z walk
+  kFlagTree = 64,     // deferred slot of a refined trial: its density is in Work::dens
 };
 constexpr int kFlagErrors = kFlagDepth | kFlagBudget;
 

@@ -138,12 +138,16 @@ __device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp,
 // deferred trials on its first lanes.
 // Returns whether the chunk deferred any trial (its zero-count word then
 // carries kZeroDefer, which finalize reports).
-__device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag) {
+// A kFlagTree slot carries the refined trial's density (dens); fold_kernel
+// settles the others.
+__device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag,
+                                   double dens = 0.0) {
   const unsigned long long b = __ballot(defer);
+  const int64_t slot = c * 64 + __popcll(b & lanemask_lt(lane));
   if (defer) {
-    const int64_t slot = c * 64 + __popcll(b & lanemask_lt(lane));
     W.wl[slot] = (unsigned char)lane;
     W.rflag[slot] = rflag;
+    if (rflag & kFlagTree) W.dens[slot] = dens;
   }
   if (lane == 0) W.wl_n[c] = __popcll(b);
   return b != 0ull;
@@ -216,6 +220,11 @@ void fast_kernel(TrialArgs A, Work W) {
 #ifndef WFPT_ENG_BLOCK
 #define WFPT_ENG_BLOCK 256
 #endif
+// waves per SIMD the engine kernel is built for (its LDS, 4 x 13.4 KB per
+// block, allows 3; its registers fit 2 without spilling)
+#ifndef WFPT_ENG_WAVES
+#define WFPT_ENG_WAVES 2
+#endif
 #ifndef WFPT_HEAVY_Z
 #define WFPT_HEAVY_Z 96
 #endif
@@ -230,7 +239,6 @@ constexpr int kFlagStop = kFlagExact | kFlagFallback | kFlagIdle;
 template <int TW>
 struct ChunkLds {
   double F[kTreePoints * 64];              // tree values: point * 64 + owner lane
-  double ZV[16 * TW * kTreePoints];        // the current round's z walks
   double X[64];                            // the owners' x
   EngTables tab;                           // the call's tables
   int fl[64];                              // the owners' flags
@@ -352,6 +360,7 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
             (MODE == kAdaptZ) ? cl.tab.zP[cl.X[tid] > 0] : cl.tab.tP;
         int fl = 0, nref = 0;
         (void)tree17(f, P, se, depth, L, fl, need, nref);
+        if (L == 0 && need) atomicOr(&cl.fl[tid], (int)kFlagRefined);
         if (L == kTreeDepth && need) fl |= kFlagFallback;  // deeper than the in-wave levels
         if (fl & (kFlagExact | kFlagFallback)) {
           atomicOr(&cl.fl[tid], fl & (kFlagExact | kFlagFallback));
@@ -470,25 +479,34 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
           if (COUNT) atomicAdd(&cl.cnt[owner], 5);
         }
       }
-      if (MODE == kAdaptTZ) team_push(pend && on, owner | (pos << 6), cl.ZQ, &cl.qn[1]);
+      if (MODE == kAdaptTZ) {
+        if (pend && on && L == 0) atomicOr(&cl.fl[owner], (int)kFlagRefined);
+        team_push(pend && on, owner | (pos << 6), cl.ZQ, &cl.qn[1]);
+      }
       ++pc.nt;
     } else if (MODE == kAdaptTZ) {
-      if (on) {
-        const double izf = cl.tab.iz[flip];
-        double* zv = cl.ZV + zslot * kTreePoints;
+      static_assert(TW == 1, "z walks gather their values by wave shuffles");
+      // lane t < 16 runs walk t: its 17 values come from lanes 4t .. 4t + 3
+      // (grid gs = source lane & 3; grid_point / grid_owns), by shuffles
+      const double izf = on ? cl.tab.iz[flip] : 0.0;
+      double yz[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j)
-          if (grid_owns(gs, j)) zv[grid_point(gs, j)] = y[j] * izf;
+      for (int j = 0; j < 5; ++j) yz[j] = y[j] * izf;
+      const int b4 = (tid & 15) * 4;
+      double zv[kTreePoints];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) zv[4 * j] = __shfl(yz[j], b4 + kGridRoot, 64);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        zv[2 + 4 * j] = __shfl(yz[j], b4 + kGridL1, 64);
+        zv[1 + 2 * j] = __shfl(yz[j], b4 + kGridL2L, 64);
+        zv[9 + 2 * j] = __shfl(yz[j + 1], b4 + kGridL2R, 64);
       }
-      team_sync<TW>();
       const int e = r * 16 * TW + tid;
       if (tid < 16 * TW && e < nz) {
         const int code = cl.ZQ[e];
         const int ow = code & 63, ps = (code >> 6) & 31;
         if (!(cl.fl[ow] & kFlagStop)) {
-          double zv[kTreePoints];
-#pragma unroll
-          for (int k = 0; k < kTreePoints; ++k) zv[k] = cl.ZV[tid * kTreePoints + k];
           int f = 0, nref = 0;
           unsigned need = 0u;
           const double zi = tree17(zv, cl.tab.zP[cl.X[ow] > 0], se, nsz, kTreeDepth, f, need, nref);
@@ -536,15 +554,19 @@ __device__ inline void tree_density(const TrialArgs& A, const ChunkLds<TW>& cl, 
 }
 
 // Chunk outputs of the owner lanes (one wave): per-trial emit, deferred
-// slots, the chunk partial and the evaluation count.
+// slots, the chunk partial and the evaluation count. kind: kFinal (a trial
+// final at level 0: its term goes into the partial), kTree (a refined trial
+// with density p: a kFlagTree slot, folded in lane order by fold_kernel), or
+// kExact (deferred to the exact path / per-lane walk, rf).
 template <bool COUNT, int OUT>
 __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, int lane, double p,
-                                 bool defer, int rf, long long ne) {
+                                 int kind, int rf, long long ne) {
   const int64_t i = c * 64 + lane;
   double lp = 0.0;
   int zero = 0;
-  if (i < A.n && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
-  const bool anyd = defer_slots(W, c, lane, defer, rf);
+  if (i < A.n && kind == kFinal) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
+  const bool defer = i < A.n && kind != kFinal;
+  const bool anyd = defer_slots(W, c, lane, defer, kind == kTree ? (int)kFlagTree : rf, p);
   if (sum_out(OUT)) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
@@ -554,7 +576,7 @@ __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, i
     }
   }
   if (COUNT) {
-    const long long nf = wave_sum_ll((i < A.n && !defer) ? ne : 0ll);
+    const long long nf = wave_sum_ll((i < A.n && kind != kExact) ? ne : 0ll);
     if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
   }
 }
@@ -596,16 +618,20 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   const bool own = lane < kSplitTrials && i < A.n;
   double p = 0.0, lp = 0.0;
   bool defer = false;
-  int rf = kFlagExact, zero = 0;
-  if (own && !(cl.fl[lane] & kFlagIdle)) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
-  if (own && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
+  int rf = kFlagExact, zero = 0, kind = kFinal;
+  if (own && !(cl.fl[lane] & kFlagIdle)) {
+    tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+    // the unsplit chunk's level-0 outcome: final unless it refined at level 0
+    kind = defer ? kExact : ((cl.fl[lane] & kFlagRefined) ? kTree : kFinal);
+  }
+  if (own && kind == kFinal) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
   if (lane < kSplitTrials) {
     const int k = slot * 64 + sub * kSplitTrials + lane;
-    S.lp[k] = lp;
-    S.meta[k] = zero | ((int)defer << 1) | (rf << 2);
+    S.lp[k] = kind == kTree ? p : lp;  // a refined trial's density, or a final trial's term
+    S.meta[k] = zero | (kind << 1) | (rf << 3);
   }
   if (COUNT) {
-    const long long nf = wave_sum_ll((own && !defer) ? (long long)cl.cnt[lane] : 0ll);
+    const long long nf = wave_sum_ll((own && kind != kExact) ? (long long)cl.cnt[lane] : 0ll);
     if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -621,9 +647,11 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const double lpc = S.lp[slot * 64 + lane];
   const int m = S.meta[slot * 64 + lane];
-  const bool anyd = defer_slots(W, c, lane, (m >> 1) & 1, m >> 2);
+  const int mk = (m >> 1) & 3;
+  const bool anyd = defer_slots(W, c, lane, mk != kFinal, mk == kTree ? (int)kFlagTree : (m >> 3),
+                                lpc);
   if (sum_out(OUT)) {
-    const double sum = wave_sum(lpc);
+    const double sum = wave_sum(mk == kFinal ? lpc : 0.0);
     const int zs = __popcll(__ballot((m & 1) != 0));
     if (lane == 0) {
       A.out[c] = sum;
@@ -635,16 +663,11 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
     record_heavy(S, c, znc > kHeavyZ);
     S.done[slot] = 0;
     S.zn[slot] = 0;
-    if (W.redo) W.redo[c] = 0;  // state pass: the lean pass flagged the split chunk
   }
 }
 
-// STATE (kPassState): the chunks' level 0 comes from the lean pass
-// (W.st: f, p, outcome, pending z integrals) instead of being recomputed; the
-// kernel carries no level-0 code. Only the chunks the lean pass flagged in
-// W.redo (refining, or split) run.
-template <int MODE, bool COUNT, int OUT, bool STATE = false>
-__global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work W, EngTables tab,
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(TrialArgs A, Work W, EngTables tab,
                                                               Split S) {
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
@@ -675,16 +698,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
     // ---- level 0, each lane its own trial, in registers ----
     double f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     unsigned pend0 = 0u;
-    if (STATE) {  // the lean pass's level 0 of this chunk (kStateWords words)
-      const double* st = W.st + c * (64 * kStateWords);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) f0[k] = st[k * 64 + lane];
-      p = st[5 * 64 + lane];
-      const long long w = __double_as_longlong(st[6 * 64 + lane]);
-      oc = own ? (int)(w & 3) : kFinal;
-      pend0 = (unsigned)((w >> 2) & 0x3fffff);
-      ne0 = w >> 24;
-    } else if (own) {
+    if (own) {
       const ZGrid G = cl.tab.G[x0 > 0][kGridRoot];
       oc = eng_level0<MODE>(x0, A.P, A.K, G, p, f0, ne0, pend0);
     }
@@ -749,10 +763,13 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
     record_heavy(S, c, nz0 > kHeavyZ);
     if (W.redo) W.redo[c] = 0;
   }
-  bool defer = oc == kExact;
-  int rf = kFlagExact;
-  if (oc == kTree) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
-  chunk_out<COUNT, OUT>(A, W, c, lane, p, defer, rf, oc == kTree ? (long long)cl.cnt[lane] : ne0);
+  int kind = oc, rf = kFlagExact;
+  if (oc == kTree) {
+    bool defer = false;
+    tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+    kind = defer ? kExact : kTree;
+  }
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, kind, rf, oc == kTree ? (long long)cl.cnt[lane] : ne0);
   pc.mark(4);
 #ifdef WFPT_PHASE_TIMING
   if (lane == 0 && c < kPhaseWaves) {
@@ -778,6 +795,15 @@ __global__ __launch_bounds__(kEngBlock, 2) void engine_kernel(TrialArgs A, Work 
 // Root z grid of boundary b (0: lower, 1: upper) with b wave-uniform: every
 // field is a select between two kernel arguments on a uniform condition, so
 // the grid stays in scalar registers.
+// WFPT_ZGRID_REF: the grid is read through a reference into the kernel
+// argument block (scalar loads at a uniform offset, on demand) instead of
+// select-copied into registers.
+#ifndef WFPT_ZGRID_REF
+#define WFPT_ZGRID_REF 1
+#endif
+#if WFPT_ZGRID_REF
+__device__ inline const ZGrid& zgrid_uniform(const RootGrids& R, int b) { return R.G[b]; }
+#else
 __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
   const ZGrid& g0 = R.G[0];
   const ZGrid& g1 = R.G[1];
@@ -797,6 +823,7 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
   G.cd = b ? g1.cd : g0.cd;
   return G;
 }
+#endif
 
 // WFPT_SIN_TABLE=0: the lean pass evaluates the large-time sines per lane
 // (the recurrence) instead of reading the call's table (same values).
@@ -805,11 +832,9 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 #endif
 
 // STATE (kPassState, the sequence predicted for data that refines): level 0
-// keeps its node values (KEEP_F) and a refining chunk leaves its lanes'
-// level-0 state in W.st for the engine's state pass instead of nothing; the
-// dataset's heavy chunks (W.pred, split by the engine) are skipped; every
-// chunk's next-call split record starts at 0 (the engine records the heavy
-// ones).
+// keeps its node values (KEEP_F); every chunk is finished the way the engine
+// finishes it (chunk_out), its refining trials becoming kFlagTree slots and
+// records {slot, level-0 state} that records_kernel completes.
 template <int MODE, bool COUNT, int OUT, bool STATE = false>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
@@ -822,16 +847,6 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
   if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
-  if (STATE) {
-    if (lane == 0 && W.next_pred) W.next_pred[c] = 0;
-    if (W.pred && W.pred[c]) {  // split by the engine's state pass
-      if (lane == 0) {
-        W.redo[c] = 1;
-        if (sum_out(OUT)) A.zeros[c] = kZeroDefer;
-      }
-      return;
-    }
-  }
   const bool own = i < A.n;
   const double x0 = own ? A.x[i] : 0.0;
   double p = 0.0, f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -856,15 +871,32 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
       oc = eng_level0_t<MODE, STATE, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
                                      ne0, pend0, WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
   }
-  if (__ballot(oc == kTree) != 0ull) {
-    if (STATE) {
-      double* st = W.st + c * (64 * kStateWords);
+  if (STATE) {
+    const unsigned long long tb = __ballot(oc == kTree);
+    if (tb) {
+      // records of the refining trials: slot (their deferred slots, as
+      // chunk_out numbers them: the rank among the chunk's deferred lanes)
+      // and level-0 state
+      const unsigned long long db = __ballot(oc != kFinal);
+      int base = 0;
+      if (lane == 0) {
+        base = atomicAdd(W.nrec, __popcll(tb));
+        atomicAdd(W.tree_any, 1);
+      }
+      base = __shfl(base, 0, 64);
+      if (oc == kTree) {
+        const int r = base + __popcll(tb & lanemask_lt(lane));
+        W.rec[r] = (int)(c * 64 + __popcll(db & lanemask_lt(lane)));
+        double* st = W.st + (int64_t)(r >> 6) * (64 * kStateWords) + (r & 63);
 #pragma unroll
-      for (int k = 0; k < 5; ++k) st[k * 64 + lane] = f0[k];
-      st[5 * 64 + lane] = p;
-      st[6 * 64 + lane] = __longlong_as_double((long long)oc | ((long long)pend0 << 2) |
-                                               ((long long)ne0 << 24));
+        for (int k = 0; k < 5; ++k) st[k * 64] = f0[k];
+        st[5 * 64] = __longlong_as_double((long long)pend0 | ((long long)ne0 << 24));
+      }
     }
+    chunk_out<COUNT, OUT>(A, W, c, lane, p, oc, kFlagExact, ne0);
+    return;
+  }
+  if (__ballot(oc == kTree) != 0ull) {
     if (lane == 0) {
       W.redo[c] = 1;
       // finalize reports the call as deferred: the host runs the redo pass
@@ -872,7 +904,89 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
     }
     return;
   }
-  chunk_out<COUNT, OUT>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, oc, kFlagExact, ne0);
+}
+
+// Records sequence (kPassState): the refining trials the state lean pass
+// listed, 64 per wave whatever their chunks (owners are independent trials
+// of one parameter set): level 0 from the record, the engine's refinement
+// rounds and tree17 (refine_rounds, tree_density), then the density into the
+// trial's kFlagTree slot, or the slot re-flagged for the exact path / the
+// per-lane walk. fold_kernel adds the slots' terms to their chunks in lane
+// order.
+// WFPT_REC_WAVES: waves per SIMD the records kernel is built for (its LDS,
+// 4 x 13.4 KB per block, allows 3); WFPT_REC_MIN: the fewest records a wave
+// takes (WFPT_REC_GRID blocks of 4 waves share the call's records)
+#ifndef WFPT_REC_WAVES
+#define WFPT_REC_WAVES 3
+#endif
+#ifndef WFPT_REC_MIN
+#define WFPT_REC_MIN 4
+#endif
+#ifndef WFPT_REC_GRID
+#define WFPT_REC_GRID 4096
+#endif
+constexpr int kRecMin = WFPT_REC_MIN;
+template <int MODE>
+__global__ __launch_bounds__(kEngBlock, WFPT_REC_WAVES) void records_kernel(TrialArgs A, Work W, EngTables tab) {
+  __shared__ ChunkLds<1> lds[kEngWaves];
+  const int lane = threadIdx.x & 63;
+  ChunkLds<1>& cl = lds[threadIdx.x >> 6];
+  const int nr = *W.nrec;
+  const int nwaves = (int)gridDim.x * kEngWaves;
+  // records per wave: as many as spread the call's records over every wave
+  // of the grid, at least kRecMin (a round's latency, not its lanes, bounds
+  // sparse refinement), at most 64
+  const int per = (nr + nwaves - 1) / nwaves;
+  const int R = per < kRecMin ? kRecMin : (per > 64 ? 64 : per);
+  load_tables(cl, tab, lane);
+  for (int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
+       g * R < nr; g += nwaves) {
+    const int r = g * R + lane;
+    const bool own = lane < R && r < nr;
+    int slot = 0;
+    double x0 = 0.0;
+    double f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    unsigned pend0 = 0u;
+    if (own) {
+      slot = W.rec[r];
+      x0 = A.x[(int64_t)(slot >> 6) * 64 + W.wl[slot]];
+      const double* st = W.st + (int64_t)(r >> 6) * (64 * kStateWords) + (r & 63);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) f0[k] = st[k * 64];
+      pend0 = (unsigned)(__double_as_longlong(st[5 * 64]) & 0xffffff);
+    }
+    cl.X[lane] = x0;
+    cl.fl[lane] = own ? 0 : (int)kFlagIdle;
+    if (own) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j) cl.F[j * (kTreeW / 4) * 64 + lane] = f0[j];
+    }
+    if (lane == 0) {
+      cl.qn[0] = 0;
+      cl.qn[1] = 0;
+    }
+    wave_sync();
+    if (MODE == kAdaptTZ) {
+#pragma unroll
+      for (int j = 0; j < 5; ++j)
+        team_push(own && ((pend0 >> (j * (kTreeW / 4))) & 1u), lane | ((j * (kTreeW / 4)) << 6),
+                  cl.ZQ, &cl.qn[1]);
+    }
+    wave_sync();
+    Tally ty;
+    PhaseClock pc;
+    refine_rounds<MODE, false, 1>(A, cl, lane, 1, ty, pc);
+    bool defer = false;
+    if (own) {
+      double p = 0.0;
+      int rf = kFlagExact;
+      tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+      if (defer) W.rflag[slot] = rf;
+      else W.dens[slot] = p;
+    }
+    wave_sync();  // the next group reuses this wave's LDS
+  }
 }
 
 // A node's trial term: mixture with the node's p_outlier, -inf for a zero
@@ -979,47 +1093,47 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
   }
 }
 
-// Settles every deferred trial and folds it into its chunk: block g walks
-// chunks g, g + G, ... (64 chunk counts per parallel load); a chunk's deferred
-// trials run on its first lanes (the exact path, or the per-lane walk for
-// deeper trees). OUT_SUM: chunk partial += wave sum of the deferred log
-// densities (fixed lane order).
+// Folds every chunk's deferred trials into it, one wave per chunk: slot k of
+// chunk c (its k-th deferred lane) on lane k; its density from dens (a
+// refined trial's, kFlagTree) or settled here (the exact path for near-ties,
+// ambiguous series decisions and subnormal densities; the per-lane walk for
+// trees deeper than kTreeDepth); the mixture and log (emit), and the wave sum
+// added to the chunk's partial (a fixed order). Resets the records counter
+// (its consumer ran before, in stream order).
 template <int MODE, bool COUNT, int OUT>
-__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw) {
-  const int lane = threadIdx.x;
-  const int64_t G = gridDim.x;
+__global__ __launch_bounds__(256, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw) {
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) W.nrec[0] = 0;
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
   long long ne = 0;
   int errf = 0;
-  for (int64_t b0 = blockIdx.x; b0 < nw; b0 += 64 * G) {
-    const int64_t myc = b0 + lane * G;
-    const int mycnt = myc < nw ? W.wl_n[myc] : 0;
-    unsigned long long work = __ballot(mycnt != 0);
-    while (work) {
-      const int j = __ffsll((long long)work) - 1;
-      work &= work - 1;
-      const int ntot = __shfl(mycnt, j, 64);
-      const int64_t c = b0 + (int64_t)j * G;
-      double lp = 0.0;
-      int zero = 0;
-      if (lane < ntot) {
-        const int64_t slot = c * 64 + lane;
-        const int64_t i = c * 64 + W.wl[slot];
-        const double x = A.x[i];
-        const int fl = W.rflag[slot];
+  for (int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < nw; c += nwaves) {
+    const int ntot = W.wl_n[c];
+    if (ntot == 0) continue;  // wave-uniform
+    double lp = 0.0;
+    int zero = 0;
+    if (lane < ntot) {
+      const int64_t slot = c * 64 + lane;
+      const int64_t i = c * 64 + W.wl[slot];
+      const int fl = W.rflag[slot];
+      double p;
+      if (fl & kFlagTree) {
+        p = W.dens[slot];  // counted where it was refined
+      } else {
         long long n1 = 0;
-        const double p = (fl & kFlagExact) ? exact_pdf(x, A.P, A.K, &n1, &errf)
-                                           : fallback_pdf<MODE>(x, A.P, A.K, &n1, &errf);
+        p = (fl & kFlagExact) ? exact_pdf(A.x[i], A.P, A.K, &n1, &errf)
+                              : fallback_pdf<MODE>(A.x[i], A.P, A.K, &n1, &errf);
         ne += n1;
-        emit<OUT>(A, i, p, lp, zero);
         if (COUNT) atomicAdd(&W.prof[(fl & kFlagExact) ? 5 : 6], 1);
       }
-      if (sum_out(OUT)) {
-        lp = wave_sum(lp);
-        const int zs = __popcll(__ballot(zero != 0));
-        if (lane == 0) {
-          A.out[c] = A.out[c] + lp;
-          A.zeros[c] = A.zeros[c] + zs;
-        }
+      emit<OUT>(A, i, p, lp, zero);
+    }
+    if (sum_out(OUT)) {
+      lp = wave_sum(lp);
+      const int zs = __popcll(__ballot(zero != 0));
+      if (lane == 0) {
+        A.out[c] = A.out[c] + lp;
+        A.zeros[c] = A.zeros[c] + zs;
       }
     }
   }
@@ -1841,11 +1955,8 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
     root_grids(A.P, R);
     if constexpr (kHasState<COUNT, OUT>) {
       if (state) {
-        Work Ws = W;
-        Ws.pred = S.n > 0 ? S.pred : nullptr;
-        Ws.next_pred = S.next_pred;
         hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT, true>), dim3(fast_blocks(A.n)),
-                           dim3(kFastBlock), 0, s, A, Ws, R);
+                           dim3(kFastBlock), 0, s, A, W, R);
         if (fast_done) (void)hipEventRecord(fast_done, s);
         return;
       }
@@ -1866,22 +1977,18 @@ static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, 
                          bool redo, bool state, hipStream_t s) {
   const int64_t nw = (A.n + 63) / 64;
   if constexpr (MODE != kDirect) {
-    if constexpr (kHasState<COUNT, OUT>) {
-      if (state) {  // the flagged chunks from their lean-pass state, the split units first
-        const int64_t units = (int64_t)S.n * kSplit + nw;
-        hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT, true>),
-                           dim3((units + kEngWaves - 1) / kEngWaves), dim3(kEngBlock), 0, s, A, W,
-                           T, S);
-        redo = false;
-      }
+    if (state) {  // the records of the refining trials, 64 per wave
+      const int64_t g = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, WFPT_REC_GRID);
+      hipLaunchKernelGGL((records_kernel<MODE>), dim3(g), dim3(kEngBlock), 0, s, A, W, T);
+      redo = false;
     }
     if (redo)  // the engine over the chunks the lean pass flagged (one wave each)
       hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>), dim3((nw + kEngWaves - 1) / kEngWaves),
                          dim3(kEngBlock), 0, s, A, W, T, Split{});
   }
-  // fold: one wave per chunk up to WFPT_FOLD_GRID waves
-  const int64_t gf = std::min<int64_t>(WFPT_FOLD_GRID, nw);
-  hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(64), 0, s, A, W, nw);
+  // the fold: one wave per chunk, up to WFPT_FOLD_GRID blocks of 4
+  const int64_t gf = std::min<int64_t>(WFPT_FOLD_GRID, (nw + 3) / 4);
+  hipLaunchKernelGGL((fold_kernel<MODE, COUNT, OUT>), dim3(gf), dim3(256), 0, s, A, W, nw);
 }
 
 template <bool COUNT, int OUT>
@@ -1897,8 +2004,11 @@ static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, c
   // launch processes every chunk); the host never combines kPassRedo with a
   // full engine level-0 pass
   Work F = W;
-  F.redo = (part & (kPassLean | kPassRedo)) || state ? W.redo : nullptr;
-  if (!state) F.st = nullptr;
+  F.redo = (part & (kPassLean | kPassRedo)) ? W.redo : nullptr;
+  if (!state) {
+    F.st = nullptr;
+    F.rec = nullptr;
+  }
 #define FAST_AND_DEFERRED(M_)                                                       \
   do {                                                                              \
     if (part & kPassFast)                                                           \

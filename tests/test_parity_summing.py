@@ -126,39 +126,69 @@ def test_lean_kernel_per_trial_on_bench_dataset(gpu, oracle_lib):
     assert dmax < 1e-9  # observed ~1e-14: far inside the bar
 
 
+def _ctx_with(env):
+    """A fresh context opened under the given WFPT_* settings (read at open)."""
+    from hddm_amd import _lib
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return _lib.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("k", range(4))
-def test_stress_sets_per_trial_engine_and_lean(gpu, oracle_lib, monkeypatch, k):
-    """The refining stress sets per trial along both sequences: the engine
-    (its level 0, in-wave rounds, heavy-chunk split units from the third call,
-    fold) and the lean pass + engine redo of the flagged chunks
-    (WFPT_LEAN_TREE=1: lean predicted whatever refined). Totals of the two
-    contexts are bitwise equal."""
+def test_stress_sets_per_trial_every_sequence(gpu, oracle_lib, k):
+    """The stress sets (parameters that refine) per trial and per chunk along
+    every call sequence a refining dataset can take: the records sequence (the
+    default once refinement is predicted: lean level 0 keeping state, the
+    refining trials 64 per wave, exact list, fold), the chunk engine
+    (WFPT_STATE=0: in-wave rounds, heavy-chunk split units from the third
+    call), and the lean pass + the engine's redo of the flagged chunks
+    (WFPT_LEAN_TREE=1). Their totals are bitwise equal."""
     from hddm_amd import _lib
     p = STRESS[k]
     np.random.seed(100 + k)
     x = gpu.gen_rts_from_cdf(*p, samples=250_000, dt=1e-3)
     ref = ref_terms(oracle_lib, x, p)
-    ctx = _lib.context()
+    tots = {}
+    for name, env, need in (("engine", None, None), ("records", {"WFPT_STATE": "1"}, "state"),
+                            ("lean+redo", {"WFPT_LEAN_TREE": "1.0"}, "lean")):
+        ctx = _lib.context() if env is None else _ctx_with(env)
+        ds = gpu.Dataset(x, ctx=ctx)
+        ds.wiener_like(*p, *KN)
+        ds.wiener_like(*p, *KN)  # the engine records heavy chunks for the next call's split
+        tot, terms, path = summing_vs_trials(ctx, ds, p)
+        if need:
+            assert need in path_names(path), (name, path_names(path))
+        assert_terms(terms, ref, f"stress {k} {name} {path_names(path)}")
+        assert_chunks(ctx, ds, ref, f"stress {k} {name}")
+        tots[name] = tot
+        ds.close()
+        if env is not None:
+            ctx.close()
+    assert len(set(tots.values())) == 1, tots
+
+
+@pytest.mark.gpu
+def test_dataset_outliving_its_context(gpu):
+    """Closing a context detaches its datasets (their device memory is
+    released with it); destroying one afterwards frees only its host part and
+    leaves no error behind for the next call, and using it fails loudly."""
+    ctx = _ctx_with({})
+    x = np.linspace(0.4, 2.0, 1000) * np.where(np.arange(1000) % 2, 1, -1)
     ds = gpu.Dataset(x, ctx=ctx)
-    ds.wiener_like(*p, *KN)
-    ds.wiener_like(*p, *KN)  # records heavy chunks for the next call's split
-    tot_e, terms_e, path_e = summing_vs_trials(ctx, ds, p)
-    assert "engine" in path_names(path_e) or "lean" in path_names(path_e)
-    assert_terms(terms_e, ref, f"stress {k} engine")
-    assert_chunks(ctx, ds, ref, f"stress {k} engine")
-    monkeypatch.setenv("WFPT_LEAN_TREE", "1.0")
-    ctx_l = _lib.Context(0)
-    monkeypatch.delenv("WFPT_LEAN_TREE")
-    ds_l = gpu.Dataset(x, ctx=ctx_l)
-    ds_l.wiener_like(*p, *KN)
-    tot_l, terms_l, path_l = summing_vs_trials(ctx_l, ds_l, p)
-    assert "lean" in path_names(path_l), path_names(path_l)
-    assert tot_l == tot_e
-    assert_terms(terms_l, ref, f"stress {k} lean+redo")
-    assert_chunks(ctx_l, ds_l, ref, f"stress {k} lean+redo")
-    ds_l.close()
-    ctx_l.close()
+    ds.wiener_like(*PINNED, *KN)
+    ctx.close()
+    with pytest.raises(ValueError):
+        ds.wiener_like(*PINNED, *KN)
+    ds.close()
+    assert np.isfinite(gpu.Dataset(x).wiener_like(*PINNED, *KN))
 
 
 @pytest.fixture(scope="module")
@@ -226,8 +256,10 @@ def test_node_sized_one_launch_per_trial(gpu, oracle_lib, lean_ctx, n):
     rng = np.random.default_rng(1000 + n)
     x = rng.choice([-1.0, 1.0], n) * (0.32 + rng.gamma(2.0, 0.4, n))
     for args in (SIMPLE, PINNED, ST_ONLY, SZ_ONLY):
+        # refining data: the lean pass + the engine's redo (a refining call
+        # is never predicted level-0-only, so small_kernel is not taken)
         _both_contexts(gpu, lean_ctx, x, args, f"node-sized {n} {args}", oracle_lib,
-                       {"small"})
+                       {"small", "lean"})
 
 
 def _seed3():
