@@ -116,7 +116,7 @@ wfpt_last_path = _sig("wfpt_last_path", _I, [_VP, ctypes.POINTER(_I)])
 wfpt_wiener_like_local = _sig("wfpt_wiener_like_local", _I, [_VP, _VP, _PP, _PK, _PD])
 # WFPT_PATH_* (include/wfpt_amd.h): kernels the last likelihood call launched
 PATH_LEAN, PATH_ENGINE, PATH_SMALL, PATH_REDO = 1, 2, 4, 8
-PATH_FOLD, PATH_DIRECT, PATH_FIXED, PATH_SPLIT, PATH_STATE = 16, 32, 64, 128, 256
+PATH_FOLD, PATH_DIRECT, PATH_FIXED, PATH_SPLIT = 16, 32, 64, 128
 wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
 EXPORTED = [

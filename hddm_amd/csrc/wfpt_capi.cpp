@@ -138,10 +138,6 @@ struct wfpt_ctx {
   DevBuf<int> wl_n;          // per chunk: deferred trials
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
   DevBuf<unsigned char> redo;  // per chunk: the lean pass left it to the engine (0 at rest)
-  DevBuf<double> st;         // records sequence (kPassState): level-0 state per record
-  DevBuf<int> rec;           // ... and each record's slot
-  DevBuf<double> dens;       // per slot: densities of deferred trials
-  int* nrec = nullptr;       // device: records of the call (0 at rest)
   int* tree_any = nullptr;   // device: some chunk refined in-wave (finalize reports + clears)
   double* fin = nullptr;     // device: multi-block finalize scratch (3 x 64 doubles)
   int* fin_ticket = nullptr; // device: its last-block ticket (0 at rest)
@@ -165,7 +161,6 @@ struct wfpt_ctx {
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
   bool small = true;           // WFPT_SMALL=0: one-block calls keep the separate finalize
-  bool state = false;          // WFPT_STATE=1: refining calls run the records sequence, not the chunk engine
   // WFPT_LEAN_TREE: the largest fraction of refining chunks (last call) for
   // which the lean pass + engine redo of those chunks beats the engine over
   // every chunk
@@ -297,7 +292,6 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   HIP_TRY(c->wl.reserve(ns));
   HIP_TRY(c->wl_n.reserve(nw));
   HIP_TRY(c->rflag.reserve(ns));
-  HIP_TRY(c->dens.reserve(ns));
   if (c->redo.cap < (size_t)nw) {
     HIP_TRY(c->redo.reserve(nw));
     HIP_TRY(hipMemsetAsync(c->redo.p, 0, c->redo.cap, c->stream));
@@ -310,10 +304,6 @@ int reserve_work(wfpt_ctx* c, int64_t n, wfpt::Work* W) {
   W->prof = c->prof;
   W->phase = c->phase;
   W->nslots = ns;
-  W->dens = c->dens.p;
-  W->st = nullptr;
-  W->rec = nullptr;
-  W->nrec = c->nrec;
   return WFPT_OK;
 }
 
@@ -392,18 +382,6 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   wfpt::Work W;
   if (int rc = reserve_work(c, n, &W)) return rc;
   const bool adaptive = wfpt::has_deferred_pass(P, K);
-  if ((part & wfpt::kPassState) && engine_family(P, K)) {
-    const size_t ns = (size_t)((n + 63) / 64) * 64;
-    HIP_TRY(c->st.reserve(ns * wfpt::kStateWords));
-    HIP_TRY(c->rec.reserve(ns));
-    W.st = c->st.p;
-    W.rec = c->rec.p;
-    // 0 at rest (fold_kernel resets it); cleared here too so that a sequence
-    // cut short by an error cannot leave stale records for the next one
-    if (part & wfpt::kPassFast) HIP_TRY(hipMemsetAsync(c->nrec, 0, sizeof(int), c->stream));
-  } else {
-    part &= ~wfpt::kPassState;
-  }
   if (part & wfpt::kPassFast) c->path = 0;  // a call sequence starts
   if (c->count && (part & wfpt::kPassFast))
     HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
@@ -414,7 +392,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   // heavy-chunk splitting belongs to full engine calls (not the lean / redo
   // passes)
   const bool eng = d && d->hcount && engine_family(P, K) &&
-                   !(part & (wfpt::kPassLean | wfpt::kPassRedo | wfpt::kPassState));
+                   !(part & (wfpt::kPassLean | wfpt::kPassRedo));
   // one block of trials, level-0 pass only (direct family, or the lean pass):
   // level 0 and finalize in one launch (WFPT_SMALL=0: two launches)
   const bool level0_only = adaptive && (engine_family(P, K)
@@ -437,11 +415,10 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
   } else {
     if (part & wfpt::kPassFast)
       c->path |= direct ? WFPT_PATH_DIRECT
-                        : (part & (wfpt::kPassLean | wfpt::kPassState))
+                        : (part & wfpt::kPassLean)
                               ? WFPT_PATH_LEAN
                               : (WFPT_PATH_ENGINE | (S.n > 0 ? WFPT_PATH_SPLIT : 0));
     if (!direct && (part & wfpt::kPassRedo)) c->path |= WFPT_PATH_REDO;
-    if (part & wfpt::kPassState) c->path |= WFPT_PATH_STATE;
     if (part & wfpt::kPassDeferred) c->path |= WFPT_PATH_FOLD;
   }
   HIP_TRY(hipGetLastError());
@@ -564,13 +541,6 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
   if (c->count || n <= 0 || !wfpt::has_deferred_pass(P, K)) return -1;
   const bool eng = engine_family(P, K);
   const bool lean = eng && lean_predicted(c, d);
-  if (eng && !lean && c->state) {
-    // refinement predicted: the lean pass keeps the refining chunks' level-0
-    // state, the engine's state pass completes them (and the heavy chunks)
-    if (int rc = run_sum(c, d->x, n, P, K, c->mres_dev, wfpt::kPassAll | wfpt::kPassState, d))
-      return rc;
-    return finish_sum(c, d, P, K, out, true);  // no engine pass: no heavy-chunk record
-  }
   const bool fast = c->fast_only && d->no_defer;
   if (!lean && !fast) return -1;
   const int lp = lean ? wfpt::kPassLean : 0;
@@ -648,7 +618,6 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
   if (const char* sm = std::getenv("WFPT_SMALL")) c->small = std::strcmp(sm, "0") != 0;
-  if (const char* sm = std::getenv("WFPT_STATE")) c->state = std::strcmp(sm, "1") == 0;
   if (const char* lt = std::getenv("WFPT_LEAN_TREE")) c->lean_tree_max = std::atof(lt);
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
@@ -666,8 +635,6 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
-  if (e == hipSuccess) e = hipMalloc((void**)&c->nrec, sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->nrec, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->ar, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMemset(c->ar, 0, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin_ticket, sizeof(int));
@@ -720,10 +687,6 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->fin_ticket) (void)hipFree(c->fin_ticket);
   if (c->ar) (void)hipFree(c->ar);
   c->redo.release();
-  c->st.release();
-  c->rec.release();
-  c->dens.release();
-  if (c->nrec) (void)hipFree(c->nrec);
   if (c->evals) (void)hipFree(c->evals);
   if (c->status) (void)hipFree(c->status);
   if (c->host_status) (void)hipHostFree(c->host_status);
@@ -1313,7 +1276,7 @@ namespace {
 // launch would dispatch one wave per chunk: ~48k blocks at 12.5M trials).
 // After ar_settle, c->ar holds the rank's triple in stream order.
 struct ArState {
-  bool eng = false, lean = false, state = false, launched = false;
+  bool eng = false, lean = false, launched = false;
 };
 int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               ArState* st) {
@@ -1322,9 +1285,7 @@ int ar_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::
   st->launched = true;
   if (st->lean)
     return run_sum(c, d->x, d->n, P, K, c->mres_dev, wfpt::kPassFast | wfpt::kPassLean, d, c->ar);
-  st->state = st->eng && c->state && !c->count;
-  return run_sum(c, d->x, d->n, P, K, c->ar,
-                 st->state ? wfpt::kPassAll | wfpt::kPassState : wfpt::kPassAll, d);
+  return run_sum(c, d->x, d->n, P, K, c->ar, wfpt::kPassAll, d);
 }
 int ar_settle(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfpt::Knobs& K,
               const ArState& st) {
@@ -1341,7 +1302,7 @@ int ar_finish(wfpt_ctx* c, const wfpt_ds* d, const ArState& st, double* out) {
   wfpt::launch_publish(c->ar, c->mres_dev, ++c->seq, c->stream);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
-  split_advance(d, st.eng && !st.lean && !st.state, c->mres);
+  split_advance(d, st.eng && !st.lean, c->mres);
   const int rc = decode_sum(c, c->mres, out);
   if (rc == WFPT_OK && st.eng) note_tree(d, c->mres);
   return rc;
@@ -1455,7 +1416,7 @@ int wfpt_wiener_like_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
   double h[8];
   HIP_TRY(hipMemcpyAsync(h, c->ar, sizeof(h), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  split_advance(d, st.eng && !st.lean && !st.state, h);
+  split_advance(d, st.eng && !st.lean, h);
   if (st.eng) note_tree(d, h);
   d->no_defer = false;
   (void)finish_profile(c);

@@ -110,8 +110,6 @@ enum Flag : int {
   kFlagBudget = 2,    // more than kEvalBudget pdf_sv evaluations in one trial
   kFlagExact = 4,     // recompute on the exact path
   kFlagFallback = 8,  // tree deeper than the breadth-first levels: per-lane walk
-  kFlagRefined = 32,  // (engine rounds) the owner refined at level 0: root test or a z walk
-  kFlagTree = 64,     // deferred slot of a refined trial: its density is in Work::dens
 };
 constexpr int kFlagErrors = kFlagDepth | kFlagBudget;
 
@@ -941,8 +939,33 @@ __device__ inline double horner(double p, double r, double c) {
 #endif
 }
 
+// WFPT_EXP_ESTRIN: the degree-11 polynomial by Estrin's scheme (dependency
+// depth 4 instead of Horner's 11, three more operations): the exponentials
+// sit on the level-0 pass's longest dependency chains. Values only (the
+// rounding differs from Horner's by an ulp; decisions keep their tie band).
+#ifndef WFPT_EXP_ESTRIN
+#define WFPT_EXP_ESTRIN 0
+#endif
 __device__ inline double exp_val(double x) {
-#if WFPT_FAST_EXP
+#if WFPT_FAST_EXP && WFPT_EXP_ESTRIN
+  const double k = rint(x * 1.4426950408889634);
+  double r = fma(-k, 6.9314718055994529e-01, x);
+  r = fma(-k, 2.3190468138462996e-17, r);
+  const double r2 = r * r;
+  const double r4 = r2 * r2;
+  const double r8 = r4 * r4;
+  const double q0 = r + 1.0;
+  const double q1 = fma(1.666666666666668e-01, r, 5.000000000000019e-01);
+  const double q2 = fma(8.333333333319601e-03, r, 4.16666666664881e-02);
+  const double q3 = fma(1.9841269890047113e-04, r, 1.3888888952314775e-03);
+  const double q4 = fma(2.755724091857897e-06, r, 2.4801485482328494e-05);
+  const double q5 = fma(2.5110037605963777e-08, r, 2.763263963904103e-07);
+  const double s0 = fma(q1, r2, q0);
+  const double s1 = fma(q3, r2, q2);
+  const double s2 = fma(q5, r2, q4);
+  const double p = fma(s2, r8, fma(s1, r4, s0));
+  return ldexp(p, (int)k);
+#elif WFPT_FAST_EXP
   const double k = rint(x * 1.4426950408889634);
   double r = fma(-k, 6.9314718055994529e-01, x);
   r = fma(-k, 2.3190468138462996e-17, r);

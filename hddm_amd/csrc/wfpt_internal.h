@@ -31,21 +31,7 @@ struct Work {
   unsigned char* redo;        // [chunks]
   int* tree_any;              // device word: some chunk of the call refined (0 at rest)
   int64_t nslots;
-  // A chunk's partial is the sum of its level-0-final trials' terms; every
-  // other trial is a deferred slot whose term fold_kernel adds in lane order:
-  // a refined trial's density (kFlagTree, in dens), or the exact path /
-  // per-lane walk. The same decomposition in every call sequence.
-  double* dens;               // [nslots] densities of the kFlagTree slots
-  // Records sequence (kPassState): the lean pass keeps level 0's values and
-  // appends each refining trial as a record {slot, level-0 state}; the
-  // records kernel completes 64 records per wave. Null outside it.
-  int* rec;                   // [nslots] slot of record r
-  double* st;                 // [nslots * kStateWords] record state, 64-record groups word-major
-  int* nrec;                  // device word: records of the call (0 at rest: fold_kernel resets it)
 };
-// level-0 state of a record: f at the root t interval's 5 nodes, and
-// pend | evaluations << 24 as an integer in a double's bits
-constexpr int kStateWords = 6;
 
 constexpr int kPhaseWaves = 16384;
 
@@ -95,11 +81,7 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 // and counted as deferred), and kPassRedo runs the engine over the flagged
 // chunks (before the fold). fast_done (optional) is recorded right after the
 // level-0 / trial kernel.
-// kPassState (adaptive engine families, with kPassAll): the lean pass keeps
-// level 0's state of the refining trials as records (Work::rec / st) and the
-// records kernel completes them, 64 per wave, without recomputing level 0.
-constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPassRedo = 8,
-              kPassState = 16;
+constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPassRedo = 8;
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,

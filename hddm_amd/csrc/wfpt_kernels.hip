@@ -138,16 +138,12 @@ __device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp,
 // deferred trials on its first lanes.
 // Returns whether the chunk deferred any trial (its zero-count word then
 // carries kZeroDefer, which finalize reports).
-// A kFlagTree slot carries the refined trial's density (dens); fold_kernel
-// settles the others.
-__device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag,
-                                   double dens = 0.0) {
+__device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defer, int rflag) {
   const unsigned long long b = __ballot(defer);
   const int64_t slot = c * 64 + __popcll(b & lanemask_lt(lane));
   if (defer) {
     W.wl[slot] = (unsigned char)lane;
     W.rflag[slot] = rflag;
-    if (rflag & kFlagTree) W.dens[slot] = dens;
   }
   if (lane == 0) W.wl_n[c] = __popcll(b);
   return b != 0ull;
@@ -235,10 +231,18 @@ constexpr int kQCap = 2 * (1 << kTreeDepth) * 64;  // tasks (or z walks) of one 
 constexpr int kFlagIdle = 16;                       // lane without a trial to integrate
 constexpr int kFlagStop = kFlagExact | kFlagFallback | kFlagIdle;
 
+// WFPT_ZWALK_LDS: a z walk's 17 values are staged in LDS (ZV) for the lane
+// that runs its tree17; 0: gathered by wave shuffles (no LDS, no barrier)
+#ifndef WFPT_ZWALK_LDS
+#define WFPT_ZWALK_LDS 1
+#endif
 // LDS of one chunk under refinement by a team of TW waves.
 template <int TW>
 struct ChunkLds {
   double F[kTreePoints * 64];              // tree values: point * 64 + owner lane
+#if WFPT_ZWALK_LDS
+  double ZV[16 * TW * kTreePoints];        // the current round's z walks
+#endif
   double X[64];                            // the owners' x
   EngTables tab;                           // the call's tables
   int fl[64];                              // the owners' flags
@@ -360,7 +364,6 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
             (MODE == kAdaptZ) ? cl.tab.zP[cl.X[tid] > 0] : cl.tab.tP;
         int fl = 0, nref = 0;
         (void)tree17(f, P, se, depth, L, fl, need, nref);
-        if (L == 0 && need) atomicOr(&cl.fl[tid], (int)kFlagRefined);
         if (L == kTreeDepth && need) fl |= kFlagFallback;  // deeper than the in-wave levels
         if (fl & (kFlagExact | kFlagFallback)) {
           atomicOr(&cl.fl[tid], fl & (kFlagExact | kFlagFallback));
@@ -480,11 +483,25 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
         }
       }
       if (MODE == kAdaptTZ) {
-        if (pend && on && L == 0) atomicOr(&cl.fl[owner], (int)kFlagRefined);
         team_push(pend && on, owner | (pos << 6), cl.ZQ, &cl.qn[1]);
       }
       ++pc.nt;
     } else if (MODE == kAdaptTZ) {
+      double zv[kTreePoints];
+#if WFPT_ZWALK_LDS
+      if (on) {
+        const double izf = cl.tab.iz[flip];
+        double* zw = cl.ZV + zslot * kTreePoints;
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (grid_owns(gs, j)) zw[grid_point(gs, j)] = y[j] * izf;
+      }
+      team_sync<TW>();
+      if (tid < 16 * TW) {
+#pragma unroll
+        for (int k = 0; k < kTreePoints; ++k) zv[k] = cl.ZV[tid * kTreePoints + k];
+      }
+#else
       static_assert(TW == 1, "z walks gather their values by wave shuffles");
       // lane t < 16 runs walk t: its 17 values come from lanes 4t .. 4t + 3
       // (grid gs = source lane & 3; grid_point / grid_owns), by shuffles
@@ -493,7 +510,6 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
 #pragma unroll
       for (int j = 0; j < 5; ++j) yz[j] = y[j] * izf;
       const int b4 = (tid & 15) * 4;
-      double zv[kTreePoints];
 #pragma unroll
       for (int j = 0; j < 5; ++j) zv[4 * j] = __shfl(yz[j], b4 + kGridRoot, 64);
 #pragma unroll
@@ -502,6 +518,7 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
         zv[1 + 2 * j] = __shfl(yz[j], b4 + kGridL2L, 64);
         zv[9 + 2 * j] = __shfl(yz[j + 1], b4 + kGridL2R, 64);
       }
+#endif
       const int e = r * 16 * TW + tid;
       if (tid < 16 * TW && e < nz) {
         const int code = cl.ZQ[e];
@@ -554,19 +571,15 @@ __device__ inline void tree_density(const TrialArgs& A, const ChunkLds<TW>& cl, 
 }
 
 // Chunk outputs of the owner lanes (one wave): per-trial emit, deferred
-// slots, the chunk partial and the evaluation count. kind: kFinal (a trial
-// final at level 0: its term goes into the partial), kTree (a refined trial
-// with density p: a kFlagTree slot, folded in lane order by fold_kernel), or
-// kExact (deferred to the exact path / per-lane walk, rf).
+// slots, the chunk partial and the evaluation count.
 template <bool COUNT, int OUT>
 __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, int lane, double p,
-                                 int kind, int rf, long long ne) {
+                                 bool defer, int rf, long long ne) {
   const int64_t i = c * 64 + lane;
   double lp = 0.0;
   int zero = 0;
-  if (i < A.n && kind == kFinal) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
-  const bool defer = i < A.n && kind != kFinal;
-  const bool anyd = defer_slots(W, c, lane, defer, kind == kTree ? (int)kFlagTree : rf, p);
+  if (i < A.n && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
+  const bool anyd = defer_slots(W, c, lane, defer, rf);
   if (sum_out(OUT)) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
@@ -576,7 +589,7 @@ __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, i
     }
   }
   if (COUNT) {
-    const long long nf = wave_sum_ll((i < A.n && kind != kExact) ? ne : 0ll);
+    const long long nf = wave_sum_ll((i < A.n && !defer) ? ne : 0ll);
     if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
   }
 }
@@ -618,20 +631,16 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   const bool own = lane < kSplitTrials && i < A.n;
   double p = 0.0, lp = 0.0;
   bool defer = false;
-  int rf = kFlagExact, zero = 0, kind = kFinal;
-  if (own && !(cl.fl[lane] & kFlagIdle)) {
-    tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
-    // the unsplit chunk's level-0 outcome: final unless it refined at level 0
-    kind = defer ? kExact : ((cl.fl[lane] & kFlagRefined) ? kTree : kFinal);
-  }
-  if (own && kind == kFinal) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
+  int rf = kFlagExact, zero = 0;
+  if (own && !(cl.fl[lane] & kFlagIdle)) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+  if (own && !defer) emit<OUT>(A, i, p, lp, zero);  // invalid parameters: p = 0
   if (lane < kSplitTrials) {
     const int k = slot * 64 + sub * kSplitTrials + lane;
-    S.lp[k] = kind == kTree ? p : lp;  // a refined trial's density, or a final trial's term
-    S.meta[k] = zero | (kind << 1) | (rf << 3);
+    S.lp[k] = lp;
+    S.meta[k] = zero | ((int)defer << 1) | (rf << 2);
   }
   if (COUNT) {
-    const long long nf = wave_sum_ll((own && kind != kExact) ? (long long)cl.cnt[lane] : 0ll);
+    const long long nf = wave_sum_ll((own && !defer) ? (long long)cl.cnt[lane] : 0ll);
     if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -647,11 +656,9 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   const double lpc = S.lp[slot * 64 + lane];
   const int m = S.meta[slot * 64 + lane];
-  const int mk = (m >> 1) & 3;
-  const bool anyd = defer_slots(W, c, lane, mk != kFinal, mk == kTree ? (int)kFlagTree : (m >> 3),
-                                lpc);
+  const bool anyd = defer_slots(W, c, lane, (m >> 1) & 1, m >> 2);
   if (sum_out(OUT)) {
-    const double sum = wave_sum(mk == kFinal ? lpc : 0.0);
+    const double sum = wave_sum(lpc);
     const int zs = __popcll(__ballot((m & 1) != 0));
     if (lane == 0) {
       A.out[c] = sum;
@@ -763,13 +770,10 @@ __global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(Trial
     record_heavy(S, c, nz0 > kHeavyZ);
     if (W.redo) W.redo[c] = 0;
   }
-  int kind = oc, rf = kFlagExact;
-  if (oc == kTree) {
-    bool defer = false;
-    tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
-    kind = defer ? kExact : kTree;
-  }
-  chunk_out<COUNT, OUT>(A, W, c, lane, p, kind, rf, oc == kTree ? (long long)cl.cnt[lane] : ne0);
+  bool defer = oc == kExact;
+  int rf = kFlagExact;
+  if (oc == kTree) tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, defer, rf, oc == kTree ? (long long)cl.cnt[lane] : ne0);
   pc.mark(4);
 #ifdef WFPT_PHASE_TIMING
   if (lane == 0 && c < kPhaseWaves) {
@@ -831,11 +835,7 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 #define WFPT_SIN_TABLE 1
 #endif
 
-// STATE (kPassState, the sequence predicted for data that refines): level 0
-// keeps its node values (KEEP_F); every chunk is finished the way the engine
-// finishes it (chunk_out), its refining trials becoming kFlagTree slots and
-// records {slot, level-0 state} that records_kernel completes.
-template <int MODE, bool COUNT, int OUT, bool STATE = false>
+template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
 #if WFPT_LEAN_REVERSE
@@ -863,38 +863,13 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
   const int b = (bp == bo) ? 1 : 0;  // every trial upper: 1; otherwise lower first
   if (own && pos == (b != 0))
-    oc = eng_level0_t<MODE, STATE, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
+    oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
                                    zgrid_uniform(R, b), p, f0, ne0, pend0,
                                    WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
   if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
     if (own && pos)
-      oc = eng_level0_t<MODE, STATE, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
+      oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
                                      ne0, pend0, WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
-  }
-  if (STATE) {
-    const unsigned long long tb = __ballot(oc == kTree);
-    if (tb) {
-      // records of the refining trials: slot (their deferred slots, as
-      // chunk_out numbers them: the rank among the chunk's deferred lanes)
-      // and level-0 state
-      const unsigned long long db = __ballot(oc != kFinal);
-      int base = 0;
-      if (lane == 0) {
-        base = atomicAdd(W.nrec, __popcll(tb));
-        atomicAdd(W.tree_any, 1);
-      }
-      base = __shfl(base, 0, 64);
-      if (oc == kTree) {
-        const int r = base + __popcll(tb & lanemask_lt(lane));
-        W.rec[r] = (int)(c * 64 + __popcll(db & lanemask_lt(lane)));
-        double* st = W.st + (int64_t)(r >> 6) * (64 * kStateWords) + (r & 63);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) st[k * 64] = f0[k];
-        st[5 * 64] = __longlong_as_double((long long)pend0 | ((long long)ne0 << 24));
-      }
-    }
-    chunk_out<COUNT, OUT>(A, W, c, lane, p, oc, kFlagExact, ne0);
-    return;
   }
   if (__ballot(oc == kTree) != 0ull) {
     if (lane == 0) {
@@ -904,89 +879,7 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
     }
     return;
   }
-  chunk_out<COUNT, OUT>(A, W, c, lane, p, oc, kFlagExact, ne0);
-}
-
-// Records sequence (kPassState): the refining trials the state lean pass
-// listed, 64 per wave whatever their chunks (owners are independent trials
-// of one parameter set): level 0 from the record, the engine's refinement
-// rounds and tree17 (refine_rounds, tree_density), then the density into the
-// trial's kFlagTree slot, or the slot re-flagged for the exact path / the
-// per-lane walk. fold_kernel adds the slots' terms to their chunks in lane
-// order.
-// WFPT_REC_WAVES: waves per SIMD the records kernel is built for (its LDS,
-// 4 x 13.4 KB per block, allows 3); WFPT_REC_MIN: the fewest records a wave
-// takes (WFPT_REC_GRID blocks of 4 waves share the call's records)
-#ifndef WFPT_REC_WAVES
-#define WFPT_REC_WAVES 3
-#endif
-#ifndef WFPT_REC_MIN
-#define WFPT_REC_MIN 4
-#endif
-#ifndef WFPT_REC_GRID
-#define WFPT_REC_GRID 4096
-#endif
-constexpr int kRecMin = WFPT_REC_MIN;
-template <int MODE>
-__global__ __launch_bounds__(kEngBlock, WFPT_REC_WAVES) void records_kernel(TrialArgs A, Work W, EngTables tab) {
-  __shared__ ChunkLds<1> lds[kEngWaves];
-  const int lane = threadIdx.x & 63;
-  ChunkLds<1>& cl = lds[threadIdx.x >> 6];
-  const int nr = *W.nrec;
-  const int nwaves = (int)gridDim.x * kEngWaves;
-  // records per wave: as many as spread the call's records over every wave
-  // of the grid, at least kRecMin (a round's latency, not its lanes, bounds
-  // sparse refinement), at most 64
-  const int per = (nr + nwaves - 1) / nwaves;
-  const int R = per < kRecMin ? kRecMin : (per > 64 ? 64 : per);
-  load_tables(cl, tab, lane);
-  for (int g = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
-       g * R < nr; g += nwaves) {
-    const int r = g * R + lane;
-    const bool own = lane < R && r < nr;
-    int slot = 0;
-    double x0 = 0.0;
-    double f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    unsigned pend0 = 0u;
-    if (own) {
-      slot = W.rec[r];
-      x0 = A.x[(int64_t)(slot >> 6) * 64 + W.wl[slot]];
-      const double* st = W.st + (int64_t)(r >> 6) * (64 * kStateWords) + (r & 63);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) f0[k] = st[k * 64];
-      pend0 = (unsigned)(__double_as_longlong(st[5 * 64]) & 0xffffff);
-    }
-    cl.X[lane] = x0;
-    cl.fl[lane] = own ? 0 : (int)kFlagIdle;
-    if (own) {
-#pragma unroll
-      for (int j = 0; j < 5; ++j) cl.F[j * (kTreeW / 4) * 64 + lane] = f0[j];
-    }
-    if (lane == 0) {
-      cl.qn[0] = 0;
-      cl.qn[1] = 0;
-    }
-    wave_sync();
-    if (MODE == kAdaptTZ) {
-#pragma unroll
-      for (int j = 0; j < 5; ++j)
-        team_push(own && ((pend0 >> (j * (kTreeW / 4))) & 1u), lane | ((j * (kTreeW / 4)) << 6),
-                  cl.ZQ, &cl.qn[1]);
-    }
-    wave_sync();
-    Tally ty;
-    PhaseClock pc;
-    refine_rounds<MODE, false, 1>(A, cl, lane, 1, ty, pc);
-    bool defer = false;
-    if (own) {
-      double p = 0.0;
-      int rf = kFlagExact;
-      tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
-      if (defer) W.rflag[slot] = rf;
-      else W.dens[slot] = p;
-    }
-    wave_sync();  // the next group reuses this wave's LDS
-  }
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
 }
 
 // A node's trial term: mixture with the node's p_outlier, -inf for a zero
@@ -1094,16 +987,13 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
 }
 
 // Folds every chunk's deferred trials into it, one wave per chunk: slot k of
-// chunk c (its k-th deferred lane) on lane k; its density from dens (a
-// refined trial's, kFlagTree) or settled here (the exact path for near-ties,
-// ambiguous series decisions and subnormal densities; the per-lane walk for
-// trees deeper than kTreeDepth); the mixture and log (emit), and the wave sum
-// added to the chunk's partial (a fixed order). Resets the records counter
-// (its consumer ran before, in stream order).
+// chunk c (its k-th deferred lane) on lane k, settled on the exact path
+// (near-ties, ambiguous series decisions, subnormal densities) or the per-lane
+// walk (trees deeper than kTreeDepth); the mixture and log (emit), and the
+// wave sum added to the chunk's partial (a fixed order).
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(256, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw) {
   const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) W.nrec[0] = 0;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   long long ne = 0;
   int errf = 0;
@@ -1116,16 +1006,11 @@ __global__ __launch_bounds__(256, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A,
       const int64_t slot = c * 64 + lane;
       const int64_t i = c * 64 + W.wl[slot];
       const int fl = W.rflag[slot];
-      double p;
-      if (fl & kFlagTree) {
-        p = W.dens[slot];  // counted where it was refined
-      } else {
-        long long n1 = 0;
-        p = (fl & kFlagExact) ? exact_pdf(A.x[i], A.P, A.K, &n1, &errf)
-                              : fallback_pdf<MODE>(A.x[i], A.P, A.K, &n1, &errf);
-        ne += n1;
-        if (COUNT) atomicAdd(&W.prof[(fl & kFlagExact) ? 5 : 6], 1);
-      }
+      long long n1 = 0;
+      const double p = (fl & kFlagExact) ? exact_pdf(A.x[i], A.P, A.K, &n1, &errf)
+                                         : fallback_pdf<MODE>(A.x[i], A.P, A.K, &n1, &errf);
+      ne += n1;
+      if (COUNT) atomicAdd(&W.prof[(fl & kFlagExact) ? 5 : 6], 1);
       emit<OUT>(A, i, p, lp, zero);
     }
     if (sum_out(OUT)) {
@@ -1940,27 +1825,15 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
   return A;
 }
 
-// the state sequence's kernels exist for the summing outputs without counting
-template <bool COUNT, int OUT>
-constexpr bool kHasState = !COUNT && sum_out(OUT);
-
 template <int MODE, bool COUNT, int OUT>
 static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
-                     bool lean, bool state, hipStream_t s, hipEvent_t fast_done) {
+                     bool lean, hipStream_t s, hipEvent_t fast_done) {
   if constexpr (MODE == kDirect) {
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W);
-  } else if (lean || state) {
+  } else if (lean) {
     RootGrids R;
     root_grids(A.P, R);
-    if constexpr (kHasState<COUNT, OUT>) {
-      if (state) {
-        hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT, true>), dim3(fast_blocks(A.n)),
-                           dim3(kFastBlock), 0, s, A, W, R);
-        if (fast_done) (void)hipEventRecord(fast_done, s);
-        return;
-      }
-    }
     hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
                        0, s, A, W, R);
   } else {
@@ -1973,15 +1846,10 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
 }
 
 template <int MODE, bool COUNT, int OUT>
-static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
-                         bool redo, bool state, hipStream_t s) {
+static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, bool redo,
+                         hipStream_t s) {
   const int64_t nw = (A.n + 63) / 64;
   if constexpr (MODE != kDirect) {
-    if (state) {  // the records of the refining trials, 64 per wave
-      const int64_t g = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, WFPT_REC_GRID);
-      hipLaunchKernelGGL((records_kernel<MODE>), dim3(g), dim3(kEngBlock), 0, s, A, W, T);
-      redo = false;
-    }
     if (redo)  // the engine over the chunks the lean pass flagged (one wave each)
       hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>), dim3((nw + kEngWaves - 1) / kEngWaves),
                          dim3(kEngBlock), 0, s, A, W, T, Split{});
@@ -1996,25 +1864,19 @@ static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, c
                         hipStream_t s, hipEvent_t fast_done) {
   // the engine's tables (the lean pass alone needs only its root grids)
   EngTables T;
-  const bool state = (part & kPassState) != 0 && W.st != nullptr;
-  const bool engine =
-      ((part & kPassFast) && !(part & kPassLean)) || (part & kPassRedo) || state;
+  const bool engine = ((part & kPassFast) && !(part & kPassLean)) || (part & kPassRedo);
   if (mode >= kAdaptT && mode <= kAdaptTZ && engine) eng_tables(A.P, T);
-  // W.redo is live only in the lean, redo and state passes (a full engine
+  // W.redo is live only in the lean and redo passes (a full engine
   // launch processes every chunk); the host never combines kPassRedo with a
   // full engine level-0 pass
   Work F = W;
   F.redo = (part & (kPassLean | kPassRedo)) ? W.redo : nullptr;
-  if (!state) {
-    F.st = nullptr;
-    F.rec = nullptr;
-  }
 #define FAST_AND_DEFERRED(M_)                                                       \
   do {                                                                              \
     if (part & kPassFast)                                                           \
-      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, state, s, fast_done); \
+      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, s, fast_done);        \
     if (part & kPassDeferred)                                                       \
-      run_deferred<M_, COUNT, OUT>(A, F, T, S, (part & kPassRedo) != 0, state, s);  \
+      run_deferred<M_, COUNT, OUT>(A, F, T, (part & kPassRedo) != 0, s);            \
   } while (0)
   switch (mode) {
     case kDirect: FAST_AND_DEFERRED(kDirect); break;

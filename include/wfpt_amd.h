@@ -264,7 +264,6 @@ int wfpt_debug_partials(wfpt_ctx *ctx, double *part, int32_t *zero, int64_t n);
 #define WFPT_PATH_DIRECT 32  /* simple-DDM level 0 (fast_kernel) */
 #define WFPT_PATH_FIXED 64   /* fixed Simpson (trial_kernel) */
 #define WFPT_PATH_SPLIT 128  /* heavy chunks split into one-wave units */
-#define WFPT_PATH_STATE 256  /* lean pass kept level-0 state; engine state pass */
 int wfpt_last_path(wfpt_ctx *ctx, int *path);
 int wfpt_synchronize(wfpt_ctx *ctx);
 

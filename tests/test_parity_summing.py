@@ -85,7 +85,7 @@ def path_names(bits):
     from hddm_amd import _lib
     names = {_lib.PATH_LEAN: "lean", _lib.PATH_ENGINE: "engine", _lib.PATH_SMALL: "small",
              _lib.PATH_REDO: "redo", _lib.PATH_FOLD: "fold", _lib.PATH_DIRECT: "direct",
-             _lib.PATH_FIXED: "fixed", _lib.PATH_SPLIT: "split", _lib.PATH_STATE: "state"}
+             _lib.PATH_FIXED: "fixed", _lib.PATH_SPLIT: "split"}
     return {v for k, v in names.items() if bits & k}
 
 
@@ -145,20 +145,18 @@ def _ctx_with(env):
 @pytest.mark.parametrize("k", range(4))
 def test_stress_sets_per_trial_every_sequence(gpu, oracle_lib, k):
     """The stress sets (parameters that refine) per trial and per chunk along
-    every call sequence a refining dataset can take: the records sequence (the
-    default once refinement is predicted: lean level 0 keeping state, the
-    refining trials 64 per wave, exact list, fold), the chunk engine
-    (WFPT_STATE=0: in-wave rounds, heavy-chunk split units from the third
-    call), and the lean pass + the engine's redo of the flagged chunks
-    (WFPT_LEAN_TREE=1). Their totals are bitwise equal."""
+    every call sequence a refining dataset can take: the chunk engine (the
+    default once refinement is predicted: in-wave rounds, heavy-chunk split
+    units from the third call, fold), and the lean pass + the engine's redo of
+    the flagged chunks (WFPT_LEAN_TREE=1). Their totals are bitwise equal."""
     from hddm_amd import _lib
     p = STRESS[k]
     np.random.seed(100 + k)
     x = gpu.gen_rts_from_cdf(*p, samples=250_000, dt=1e-3)
     ref = ref_terms(oracle_lib, x, p)
     tots = {}
-    for name, env, need in (("engine", None, None), ("records", {"WFPT_STATE": "1"}, "state"),
-                            ("lean+redo", {"WFPT_LEAN_TREE": "1.0"}, "lean")):
+    for name, env, need in (("engine", None, "engine"), ("lean+redo", {"WFPT_LEAN_TREE": "1.0"},
+                                                         "lean")):
         ctx = _lib.context() if env is None else _ctx_with(env)
         ds = gpu.Dataset(x, ctx=ctx)
         ds.wiener_like(*p, *KN)

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 OUT=gpurun_out/r04/ab
 mkdir -p $OUT
-VARIANTS=${VARIANTS:-"default eng3 records zref"}
+VARIANTS=${VARIANTS:-"default zshfl estrin"}
 for rep in 1 2; do
   for v in $VARIANTS; do
     case $v in
