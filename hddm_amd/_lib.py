@@ -114,6 +114,9 @@ wfpt_debug_partials = _sig("wfpt_debug_partials", _I,
                            [_VP, _PD, ctypes.POINTER(ctypes.c_int32), _I64])
 wfpt_last_path = _sig("wfpt_last_path", _I, [_VP, ctypes.POINTER(_I)])
 wfpt_wiener_like_local = _sig("wfpt_wiener_like_local", _I, [_VP, _VP, _PP, _PK, _PD])
+wfpt_wiener_like_nodes_local = _sig("wfpt_wiener_like_nodes_local", _I, [_VP, _VP, _PP, _PK, _PD])
+wfpt_wiener_like_nodes_allreduce = _sig("wfpt_wiener_like_nodes_allreduce", _I,
+                                        [_VP, _VP, _PP, _PK, _PD])
 # WFPT_PATH_* (include/wfpt_amd.h): kernels the last likelihood call launched
 PATH_LEAN, PATH_ENGINE, PATH_SMALL, PATH_REDO = 1, 2, 4, 8
 PATH_FOLD, PATH_DIRECT, PATH_FIXED, PATH_SPLIT = 16, 32, 64, 128
@@ -130,7 +133,7 @@ EXPORTED = [
     "wfpt_comm_init_all", "wfpt_wiener_like_allreduce_group", "wfpt_result_poison",
     "wfpt_wiener_like_nodes_ex", "wfpt_wiener_like_multi_ex", "wfpt_wiener_like_multi_resident_ex",
     "wfpt_wiener_like_trials", "wfpt_dataset_order", "wfpt_debug_partials", "wfpt_last_path",
-    "wfpt_wiener_like_local",
+    "wfpt_wiener_like_local", "wfpt_wiener_like_nodes_local", "wfpt_wiener_like_nodes_allreduce",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)

@@ -981,18 +981,17 @@ int wfpt_wiener_like_nodes(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per
   return wfpt_wiener_like_nodes_ex(c, d, per_node, k, out, nullptr);
 }
 
-int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
-                              const wfpt_knobs* k, double* out, double* out_trial) {
-  if (!c || !d || !per_node || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
-  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
-  if (!d->node) return fail(WFPT_ERR_ARG, "dataset was created without node ids");
-  const wfpt::Knobs K = to_knobs(k);
-  WFPT_RANGE("wfpt_wiener_like_nodes");
-  std::lock_guard<std::mutex> lk(c->mu);
-  DeviceGuard g(c->device);
+}  // extern "C"
+
+namespace {
+// The per-node pass of a node dataset (everything before the per-node sums):
+// the parameter table into mapped pinned memory (node_fast_kernel stages the
+// rows each block needs in LDS: no H2D copy per call), the family every node
+// selects, and the level-0 / chunk-engine / record kernels writing each
+// trial's term to c->lp.
+int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
+                 const wfpt::Knobs& K) {
   const int32_t m = d->n_nodes;
-  // the parameter table goes straight into mapped pinned memory: node_kernel
-  // stages the rows each block needs in LDS (no H2D copy per call)
   HIP_TRY(c->mnodep.reserve(m));
   int mode = -2;  // the integration family every node selects, or -1 if mixed
   for (int32_t j = 0; j < m; ++j) {
@@ -1002,7 +1001,7 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   }
   if (mode > wfpt::kAdaptTZ) mode = -1;  // fixed Simpson: generic kernel
   if (c->nodes_generic) mode = -1;
-  HIP_TRY(c->res.reserve(std::max<int32_t>(m, 1)));
+  HIP_TRY(c->res.reserve((size_t)m + 1));
   if (mode >= 0) {  // deferred records / listed chunks of the per-node fast path
     HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
@@ -1018,6 +1017,29 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
                      c->status, c->prof, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  return WFPT_OK;
+}
+
+int nodes_check(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node, const wfpt_knobs* k,
+                const void* out) {
+  if (!c || !d || !per_node || !k || !out) return fail(WFPT_ERR_ARG, "null pointer");
+  if (d->ctx != c) return fail(WFPT_ERR_ARG, "dataset belongs to another context");
+  if (!d->node) return fail(WFPT_ERR_ARG, "dataset was created without node ids");
+  return WFPT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
+                              const wfpt_knobs* k, double* out, double* out_trial) {
+  if (int rc = nodes_check(c, d, per_node, k, out)) return rc;
+  const wfpt::Knobs K = to_knobs(k);
+  WFPT_RANGE("wfpt_wiener_like_nodes");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const int32_t m = d->n_nodes;
+  if (int rc = nodes_launch(c, d, per_node, K)) return rc;
   ++c->seq;
   if (m > 0) {
     // per-node sums, status and the completion word land in mapped memory
@@ -1038,6 +1060,71 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
     HIP_TRY(hipMemcpy(h.data(), c->lp.p, d->n * sizeof(double), hipMemcpyDeviceToHost));
     for (int64_t i = 0; i < d->n; ++i) out_trial[d->perm[i]] = h[i];
   }
+  return WFPT_OK;
+}
+
+int wfpt_wiener_like_nodes_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
+                                 const wfpt_knobs* k, double* out) {
+  if (int rc = nodes_check(c, d, per_node, k, out)) return rc;
+  const wfpt::Knobs K = to_knobs(k);
+  WFPT_RANGE("wfpt_wiener_like_nodes_local");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const int32_t m = d->n_nodes;
+  if (int rc = nodes_launch(c, d, per_node, K)) return rc;
+  wfpt::launch_segment_res(c->lp.p, d->off, m, c->res.p, c->status, false, c->stream);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(out, c->res.p, ((size_t)m + 1) * sizeof(double), hipMemcpyDeviceToHost,
+                         c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return finish_profile(c);
+}
+
+int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
+                                     const wfpt_knobs* k, double* out) {
+  if (!c) return fail(WFPT_ERR_ARG, "null context");
+  if (!c->comm) return fail(WFPT_ERR_ARG, "wfpt_comm_init was not called");
+  WFPT_RANGE("wfpt_wiener_like_nodes_allreduce");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  // every exit once the communicator exists goes through the exchange: a
+  // rank whose pass fails enters it with a poisoned vector
+  int lrc = nodes_check(c, d, per_node, k, out);
+  const int32_t m = d && d->ctx == c ? d->n_nodes : 0;
+  if (lrc == WFPT_OK) lrc = nodes_launch(c, d, per_node, to_knobs(k));
+  std::string lmsg = lrc != WFPT_OK ? g_last_error : std::string();
+  if (c->res.cap < (size_t)m + 1) {  // the node vector of an early failure
+    if (c->res.reserve((size_t)m + 1) != hipSuccess) {
+      (void)ncclCommAbort(c->comm);
+      c->comm = nullptr;
+      return fail(WFPT_ERR_HIP, "node all-reduce: no device buffer for the exchange "
+                                "(RCCL communicator aborted)");
+    }
+  }
+  wfpt::launch_segment_res(lrc == WFPT_OK ? c->lp.p : nullptr, d ? d->off : nullptr, m, c->res.p,
+                           c->status, lrc != WFPT_OK, c->stream);
+  if (hipGetLastError() != hipSuccess) {
+    (void)ncclCommAbort(c->comm);
+    c->comm = nullptr;
+    return fail(lrc != WFPT_OK ? lrc : WFPT_ERR_HIP,
+                lmsg + " (device stream unusable: RCCL communicator aborted)");
+  }
+  // per-node sums (and the error count) of every rank summed: a node's
+  // -inf on any rank reaches every rank (wfpt.pyx:71-72 per node)
+  const ncclResult_t nr = ncclAllReduce(c->res.p, c->res.p, (size_t)m + 1, ncclDouble, ncclSum,
+                                        c->comm, c->stream);
+  if (lrc != WFPT_OK) {
+    (void)hipStreamSynchronize(c->stream);
+    return fail(lrc, lmsg);
+  }
+  if (nr != ncclSuccess)
+    return fail(WFPT_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+  wfpt::launch_publish_vec(c->res.p, m, c->mnode.d, ++c->seq, c->stream);
+  HIP_TRY(hipGetLastError());
+  if (int rc = wait_word(c, c->mnode.h + m + 1)) return rc;
+  if (int rc = check_status_value(c->mnode.h[m])) return rc;
+  if (int rc = finish_profile(c)) return rc;
+  std::memcpy(out, c->mnode.h, m * sizeof(double));
   return WFPT_OK;
 }
 

@@ -128,6 +128,14 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
                   hipStream_t s);
 // res (device, n_nodes) per-node sums; then out (mapped host): [0, n_nodes)
 // the sums, [n_nodes] encoded error flags, [n_nodes + 1] the completion word.
+// Node all-reduce: res[0, n_nodes) per-node sums (or zeros when poison),
+// res[n_nodes] the encoded error count (kPeerFailUnit when poison; the device
+// status word is reset); then, after the exchange, res -> out[0, n_nodes] and
+// the completion word out[n_nodes + 1].
+void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
+                        int* status, bool poison, hipStream_t s);
+void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long long seq,
+                        hipStream_t s);
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s);
 // wiener_like_multi with a uniform adaptive / direct family (mode): level-0

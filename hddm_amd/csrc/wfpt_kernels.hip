@@ -1,24 +1,33 @@
 // wfpt_kernels.hip — gfx950 kernels of the WFPT likelihood engine.
 //
-// Adaptive / direct integration families (the HDDM case), one call:
-//   fast_kernel<MODE>     level-0 pass, one 64-trial chunk per wave: trials
-//                         whose root Simpson tests pass finish here (mixture,
-//                         log, per-chunk partial); the others are compacted per
-//                         chunk into tree records (refinement) or exact records
-//   gather_kernel         level-1 task list from the per-chunk counts
-//   level_kernel<MODE,L>  tree level L breadth-first over all deferred trials:
-//                         one task = one interval (2 new sample points + its
-//                         stop test), refined intervals push their children
-//   fold_kernel<MODE>     per chunk: the deferred trials' densities (tree
-//                         re-walk, exact path, per-lane fallback), mixture and
-//                         log, added to the chunk's partial in lane order
+// Adaptive / direct integration families (the HDDM case), one resident call:
+//   lean_kernel<MODE>     level 0 of every trial, one 64-trial chunk per wave,
+//                         boundary-uniform root grids in scalar registers (4
+//                         waves/SIMD): a chunk none of whose trials refines
+//                         ends here (mixture, log, chunk partial); a chunk that
+//                         refines is flagged for the engine's redo pass
+//   engine_kernel<MODE>   level 0 + in-wave refinement rounds (z walks, t-node
+//                         tasks, tree17) of a chunk per wave; heavy chunks
+//                         recorded by the previous call run as 8 split units
+//   small_kernel<MODE>    <= 256 trials (one HDDM node): level 0 and the
+//                         finalize in one launch
+//   fast_kernel<kDirect>  the simple DDM (one pdf_sv per trial)
+//   fold_kernel<MODE>     one wave per chunk: its deferred trials (exact path,
+//                         trees deeper than kTreeDepth) settled in lane
+//                         order and added to the chunk's partial
 //   finalize_kernel       fixed-order sum of the chunk partials -> mapped slot
-// The per-chunk partial of a chunk is the same value whether or not the call
-// ran the deferred kernels (a chunk without deferred trials is never touched),
-// so a likelihood is bitwise reproducible across call sequences. No float
-// atomics on any likelihood value.
-// Fixed Simpson (use_adaptive = 0): trial_kernel. Per-node and per-trial
-// parameter variants: node_*_kernel, multi_kernel.
+// The per-chunk partial of a chunk is the same value whichever sequence ran
+// it (lean, lean + redo, engine, split), so a likelihood is bitwise
+// reproducible across call histories. No float atomics on any likelihood
+// value. OUT_BOTH builds of the same kernels also write each trial's term
+// (wfpt_wiener_like_trials: the per-trial check of the summing path).
+// Fixed Simpson (use_adaptive = 0): trial_kernel. Per-node parameters
+// (wfpt_wiener_like_nodes): node_fast_kernel (level 0, LDS-staged node rows)
+// + node_chunk_kernel (listed chunks, 64 trials per wave per node segment) +
+// node_defer_kernel (exact / walk records); generic node_kernel for mixed
+// families. Per-trial parameters (wiener_like_multi): multi_fast_kernel +
+// node_engine_kernel<..., MULTI> (one wave per deferred record), or the
+// generic multi_kernel.
 #include "wfpt_device.hpp"
 #include "wfpt_internal.h"
 
@@ -1375,6 +1384,33 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
   }
 }
 
+// Node all-reduce (wfpt_wiener_like_nodes_allreduce): the encoded error
+// count of this rank's node pass appended to its per-node sums (res[n]),
+// status reset; or a failed rank's poisoned vector {0 ..., kPeerFailUnit}.
+__global__ __launch_bounds__(64) void node_status_kernel(double* res, int32_t n, int* status,
+                                                         int poison) {
+  if (threadIdx.x == 0) {
+    const int st = atomicExch(status, 0);
+    res[n] = poison ? kPeerFailUnit
+                    : (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+  }
+}
+__global__ __launch_bounds__(256) void node_poison_kernel(double* res, int32_t n) {
+  for (int j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) res[j] = 0.0;
+}
+// The all-reduced vector (n sums + the error count) to mapped memory, then
+// the completion word out[n + 1].
+__global__ __launch_bounds__(256) void publish_vec_kernel(const double* res, int32_t n,
+                                                          double* out, unsigned long long seq) {
+  for (int j = threadIdx.x; j <= n; j += 256) out[j] = res[j];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    reinterpret_cast<volatile unsigned long long*>(out + n + 1)[0] = seq;
+    __threadfence_system();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Per-node parameters (wfpt_wiener_like_nodes): trials of node j use P[j].
 // The dataset is grouped by node, so a 256-trial block spans a short run of
@@ -2059,6 +2095,24 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
     else NODE_LAUNCH(2, false);
   }
 #undef NODE_LAUNCH
+}
+
+void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
+                        int* status, bool poison, hipStream_t s) {
+  if (poison) {
+    hipLaunchKernelGGL(node_poison_kernel, dim3(std::max<int32_t>((n_nodes + 255) / 256, 1)),
+                       dim3(256), 0, s, res, n_nodes);
+  } else if (n_nodes > 0) {
+    hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
+                       n_nodes, res);
+  }
+  hipLaunchKernelGGL(node_status_kernel, dim3(1), dim3(64), 0, s, res, n_nodes, status,
+                     poison ? 1 : 0);
+}
+
+void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long long seq,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(publish_vec_kernel, dim3(1), dim3(256), 0, s, res, n, out, seq);
 }
 
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,

@@ -284,6 +284,36 @@ class Dataset:
         del keep
         return (out.value, terms) if trials else out.value
 
+    def _node_table(self, params):
+        if self.n_nodes == 0:
+            raise ValueError("dataset was created without node ids")
+        pm = np.ascontiguousarray(np.asarray(params, dtype=np.float64))
+        if pm.shape != (self.n_nodes, 8):
+            raise ValueError(f"params must have shape ({self.n_nodes}, 8)")
+        return (_lib.Params * self.n_nodes).from_buffer_copy(pm.tobytes())
+
+    def wiener_like_nodes_local(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
+                                simps_err=1e-3, w_outlier=0.1):
+        """This shard's per-node partial sums and its encoded error count
+        (n_nodes + 1 values): what wiener_like_nodes_allreduce sums over ranks."""
+        table = self._node_table(params)
+        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        out = np.empty(self.n_nodes + 1, dtype=np.float64)
+        _lib.check(_lib.wfpt_wiener_like_nodes_local(self.ctx.handle, self.handle, table,
+                                                     ctypes.byref(K), _lib.dptr(out)))
+        return out
+
+    def wiener_like_nodes_allreduce(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
+                                    simps_err=1e-3, w_outlier=0.1):
+        """Per-node sums over every rank's shard (hddm_amd.dist.init_comm):
+        one all-reduce of n_nodes + 1 doubles per call."""
+        table = self._node_table(params)
+        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        out = np.empty(self.n_nodes, dtype=np.float64)
+        _lib.check(_lib.wfpt_wiener_like_nodes_allreduce(self.ctx.handle, self.handle, table,
+                                                         ctypes.byref(K), _lib.dptr(out)))
+        return out
+
     def wiener_like_nodes(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
                           simps_err=1e-3, w_outlier=0.1, trials=False):
         """params: array (n_nodes, 8) of v, sv, a, z, sz, t, st, p_outlier.

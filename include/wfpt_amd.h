@@ -207,6 +207,22 @@ int wfpt_wiener_like_allreduce_group(wfpt_ctx *const *ctxs, const wfpt_ds *const
  * outside [0, 1] gives {0, 1, 0} (decodes to -inf). */
 int wfpt_wiener_like_local(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *p,
                            const wfpt_knobs *k, double triple[3]);
+/* Hierarchical (batched) mode across ranks ("count =
+ * n_nodes"): each rank holds a node dataset of its own trial shard with the
+ * global node ids (a node may be split over ranks or absent); its per-node
+ * partial sums plus the encoded error count (n_nodes + 1 doubles) are summed
+ * with one ncclAllReduce, and every rank receives the per-node totals of all
+ * trials in out_logp[n_nodes] (a node with a zero-density trial on any rank is
+ * -inf). Failure semantics as wfpt_wiener_like_allreduce. */
+int wfpt_wiener_like_nodes_allreduce(wfpt_ctx *ctx, const wfpt_ds *ds,
+                                     const wfpt_params *per_node, const wfpt_knobs *k,
+                                     double *out_logp);
+/* This rank's part of that exchange, for a caller with its own collective:
+ * out[n_nodes + 1] = the per-node partial sums of its shard and the encoded
+ * error count (sum over ranks, then a nonzero last entry decodes as in
+ * wfpt_decode_result's third word). */
+int wfpt_wiener_like_nodes_local(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *per_node,
+                                 const wfpt_knobs *k, double *out);
 /* The triple a rank that failed before the exchange contributes: {0, 0,
  * 2^40} (one "failed rank" unit; see wfpt_decode_result). */
 int wfpt_result_poison(double r[3]);

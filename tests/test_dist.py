@@ -341,3 +341,91 @@ def test_two_rank_gloo_with_device_triples(gpu, oracle_lib):
     kn0 = kn[:5] + (0.0, 0.1)  # p_outlier 0: a zero Wiener density is a zero mixture density
     res0 = _run(x0, None, kn0, None, worker=_device_worker, extra=[calm])
     assert all(g[0] == -math.inf for g in res0)
+
+
+def _node_worker(rank, world, port, x, node, params, kn, out_q):
+    """A rank of the hierarchical-mode exchange: its contiguous trial shard as
+    a node dataset with the global node ids, the library's per-node partial
+    sums (wfpt_wiener_like_nodes_local), summed over gloo."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from hddm_amd import _lib, wfpt
+    from hddm_amd import dist as hdist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = hdist.shard_range(x.size, world, rank)
+    ds = wfpt.Dataset(x[lo:hi], node_id=node[lo:hi], n_nodes=params.shape[0])
+    v = torch.tensor(ds.wiener_like_nodes_local(params, *kn), dtype=torch.float64)
+    dist.all_reduce(v)
+    v = v.numpy()
+    if v[-1] != 0:
+        _lib.decode_result([0.0, 0.0, float(v[-1])])
+    out_q.put((rank, v[:-1], hi - lo))
+    ds.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_gloo_node_sums(gpu, oracle_lib):
+    """Hierarchical mode across ranks (count = n_nodes): two
+    processes on the device, each with a contiguous shard of a 61-node dataset
+    (node 30 split between the ranks), their per-node partial sums summed over
+    gloo equal the unsharded per-node sums and the reference's per-node fsum;
+    a zero-density trial in a split node makes that node -inf on every rank."""
+    rng = np.random.default_rng(14)
+    m, per = 61, 150  # 9150 trials: the shard boundary 4575 splits node 30
+    node = np.repeat(np.arange(m, dtype=np.int32), per)
+    x = rng.choice([-1.0, 1.0], node.size) * (0.34 + rng.gamma(2.0, 0.4, node.size))
+    params = np.tile([0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1, 0.05], (m, 1))
+    params[:, 0] += 0.02 * np.arange(m)
+    kn = (1e-4, 2, 2, 1, 1e-3, 0.1)
+    want = gpu.Dataset(x, node_id=node, n_nodes=m).wiener_like_nodes(params, *kn)
+    for xx, zero in ((x, False), (np.where(np.arange(x.size) == 4520, 0.05, x), True)):
+        pz = params.copy()
+        if zero:
+            pz[:, 7] = 0.0  # no outlier mass: the zero density is -inf
+            want = gpu.Dataset(xx, node_id=node, n_nodes=m).wiener_like_nodes(pz, *kn)
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_node_worker, args=(r, 2, port, xx, node, pz, kn, q))
+                 for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=120) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        for _, got, _ in res:
+            fin = np.isfinite(want)
+            assert np.array_equal(np.isneginf(got), np.isneginf(want))
+            assert np.all(np.abs(got[fin] - want[fin]) <= 1e-11 * np.abs(want[fin]))
+        if zero:
+            assert np.isneginf(want[4520 // per])
+        else:
+            for j in (0, 30, 60):
+                terms = oracle_lib.pdf_array(xx[node == j], *pz[j, :7], kn[0], 1, kn[1], kn[2],
+                                             kn[3], kn[4], pz[j, 7], kn[5], n_threads=4)
+                assert abs(want[j] - math.fsum(terms)) <= 1e-11 * math.fsum(np.abs(terms))
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_node_allreduce(gpu):
+    """wfpt_wiener_like_nodes_allreduce over world-1 RCCL equals
+    wiener_like_nodes bit for bit (one all-reduce of n_nodes + 1 doubles)."""
+    from hddm_amd import _lib, dist as hdist
+    ctx = _lib.context()
+    hdist.init_comm(ctx, 0, 1)
+    rng = np.random.default_rng(15)
+    m = 40
+    node = rng.integers(0, m, 8000).astype(np.int32)
+    x = rng.choice([-1.0, 1.0], node.size) * (0.34 + rng.gamma(2.0, 0.4, node.size))
+    params = np.tile([0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1, 0.05], (m, 1))
+    ds = gpu.Dataset(x, node_id=node, n_nodes=m)
+    a = ds.wiener_like_nodes(params)
+    b = ds.wiener_like_nodes_allreduce(params)
+    assert np.array_equal(a, b)
