@@ -114,3 +114,19 @@ def test_combine_semantics():
     assert dist.combine([(-3.0, 0), (-4.5, 2)]) == -np.inf
     assert dist.combine([(float("nan"), 0), (-1.0, 1)]) == -np.inf  # zero beats NaN (wfpt.pyx:71)
     assert np.isnan(dist.combine([(float("nan"), 0), (-1.0, 0)]))
+
+
+def test_new_entry_points_reject_null_arguments_without_gpu():
+    """The r04 entry points (per-trial check, stored order, chunk partials,
+    launched path, rank-local parts, per-node all-reduce) validate their
+    arguments before touching a device: WFPT_ERR_ARG with a message."""
+    from hddm_amd import _lib
+    two = 2
+    assert _lib.wfpt_wiener_like_trials(None, None, None, None, None, None) == two
+    assert _lib.wfpt_dataset_order(None, None) == two
+    assert _lib.wfpt_debug_partials(None, None, None, 0) == two
+    assert _lib.wfpt_last_path(None, None) == two
+    assert _lib.wfpt_wiener_like_local(None, None, None, None, None) == two
+    assert _lib.wfpt_wiener_like_nodes_local(None, None, None, None, None) == two
+    assert _lib.wfpt_wiener_like_nodes_allreduce(None, None, None, None, None) == two
+    assert b"null" in _lib.wfpt_last_error()
