@@ -116,13 +116,19 @@ struct CdfTrial {
   int x, sg, sh, branch;
 };
 
+// Z_U / Z_L of boundary x (cdfdif.c:116-117): parameter-only, per boundary.
+__device__ inline void z_bounds(int x, const CdfPar& P, double& Z_U, double& Z_L) {
+  const double a = P.a, z = P.z, sZ = P.sZ;
+  Z_U = (((1 - x) * z) + (x * (a - z))) + (sZ / 2);
+  Z_L = (((1 - x) * z) + (x * (a - z))) - (sZ / 2);
+}
+
 __device__ inline CdfTrial cdf_prepare(double t, int x, const CdfPar& P, const CdfShared& S) {
-  const double a = P.a, Ter = P.Ter, sZ = P.sZ, st = P.st, z = P.z;
+  const double Ter = P.Ter, st = P.st;
   CdfTrial T;
   T.t = t;
   T.x = x;
-  T.Z_U = (((1 - x) * z) + (x * (a - z))) + (sZ / 2);
-  T.Z_L = (((1 - x) * z) + (x * (a - z))) - (sZ / 2);
+  z_bounds(x, P, T.Z_U, T.Z_L);
   T.lower_t = Ter - (st / 2);
   T.sg = 2 * x - 1;  // (2*x-1)
   T.sh = 1 - 2 * x;  // (1-2*x)
@@ -137,29 +143,50 @@ __device__ inline CdfTrial cdf_prepare(double t, int x, const CdfPar& P, const C
   return T;
 }
 
-// Term v of the series beyond the window, v * sum_nu (cdfdif.c:130-143).
-__device__ inline double beyond_term(int v, const CdfTrial& T, const CdfPar& P,
+// Term (v, m) of the series beyond the window (cdfdif.c:130-143) in three
+// factors. Beyond the window upper_t = Ter + st/2 for every trial, so only
+// exp(dh * (t - upper_t) + lx) depends on the trial: denom, dh, lx and fact
+// depend on (v, m) and the boundary x alone, and cdf_table_kernel evaluates
+// them once per call with these same helpers (bit-identical terms).
+__device__ inline double beyond_denom(int v, double g, double a2) {
+  const double pv = ((kCPi * kCPi) * (double)(v * v)) / (100 * a2);
+  return ((100 * g) * g) + pv;
+}
+
+// log(1 - exp(dh * (upper_t - lower_t))), dh = -denom/2 (cdfdif.c:141-142)
+__device__ inline double beyond_lx(double dh, double width) { return log(1 - exp(dh * width)); }
+
+// fact of (v, m) on boundary x (cdfdif.c:133-140)
+__device__ inline double beyond_fact(int v, int m, int x, double denom, const CdfPar& P,
                                      const CdfShared& S) {
-  const double a = P.a, a2 = a * a, t = T.t, upper_t = T.upper_t, lower_t = T.lower_t;
-  const double Z_U = T.Z_U, Z_L = T.Z_L;
-  const int sg = T.sg;
+  const double a = P.a;
+  double Z_U, Z_L;
+  z_bounds(x, P, Z_U, Z_L);
+  const int sg = 2 * x - 1;
   const double l100 = log(100.);
-  double sum_nu = 0;
   const double sifa = (kCPi * v) / a;
   const double sU = sin(sifa * Z_U), cU = cos(sifa * Z_U);
   const double sL = sin(sifa * Z_L), cL = cos(sifa * Z_L);
-  const double pv = ((kCPi * kCPi) * (double)(v * v)) / (100 * a2);
+  const double g = S.gk[m];
+  const double ld = 3 * log(denom);
+  const double upp = exp(((((sg * Z_U) * g) * 100) - ld + S.lw[m]) - (2 * l100));
+  const double low = exp(((((sg * Z_L) * g) * 100) - ld + S.lw[m]) - (2 * l100));
+  return (upp * ((((sg * g) * sU) * 100) - (sifa * cU))) -
+         (low * ((((sg * g) * sL) * 100) - (sifa * cL)));
+}
+
+// Term v of the series beyond the window, v * sum_nu, evaluated in full
+// (cdf_wave_kernel's terms past the per-call table).
+__device__ inline double beyond_term(int v, const CdfTrial& T, const CdfPar& P,
+                                     const CdfShared& S) {
+  const double a2 = P.a * P.a, t_up = T.t - T.upper_t, width = T.upper_t - T.lower_t;
+  double sum_nu = 0;
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
-    const double g = S.gk[m];
-    const double denom = ((100 * g) * g) + pv;
-    const double ld = 3 * log(denom);
-    const double upp = exp(((((sg * Z_U) * g) * 100) - ld + S.lw[m]) - (2 * l100));
-    const double low = exp(((((sg * Z_L) * g) * 100) - ld + S.lw[m]) - (2 * l100));
-    const double fact = (upp * ((((sg * g) * sU) * 100) - (sifa * cU))) -
-                        (low * ((((sg * g) * sL) * 100) - (sifa * cL)));
-    const double exdif = exp(((-.5 * denom) * (t - upper_t)) +
-                             log(1 - exp((-.5 * denom) * (upper_t - lower_t))));
+    const double denom = beyond_denom(v, S.gk[m], a2);
+    const double dh = -.5 * denom;
+    const double fact = beyond_fact(v, m, T.x, denom, P, S);
+    const double exdif = exp((dh * t_up) + beyond_lx(dh, width));
     sum_nu += fact * exdif;
   }
   return v * sum_nu;
@@ -228,52 +255,110 @@ __device__ inline double cdf_output(double Fnew, double xi, double p_outlier, do
   return (y * (1 - p_outlier)) + (((xi + (1. / (2 * w_outlier))) * w_outlier) * p_outlier);
 }
 
-// Per-lane pass: trials below the window, and trials beyond it whose series
-// converges within kLaneTerms terms, are finished here. The rest — window
-// trials (36 series of up to 5000 terms each) and slowly converging series
-// near the window edge — are appended to `defer` (their cost would otherwise
-// hold a whole wave) for cdf_wave_kernel.
+// Per-call tables of the series beyond the window for v < kLaneTerms, rows
+// padded to kTabRow so the two boundary rows of fact fall in different LDS
+// banks. Written by cdf_table_kernel, staged into LDS by dmat_cdf_kernel.
 constexpr int kLaneTerms = 48;
+constexpr int kTabRow = kLaneTerms + 4;
+struct CdfTable {
+  CdfShared S;
+  double dh[6][kTabRow];       // -denom(v, m) / 2
+  double lx[6][kTabRow];       // log(1 - exp(dh * st_window))
+  double fact[2][6][kTabRow];  // fact(v, m) per boundary x
+};
 
-__global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, int64_t n,
-                                                             CdfPar P, double p_outlier,
-                                                             double w_outlier, double* out,
-                                                             int* defer, int* n_defer) {
+// One block per drift node m, one lane per v: the parameter-only state
+// (cdf_setup) and the (v, m) factors of the beyond-window series.
+__global__ __launch_bounds__(64) void cdf_table_kernel(CdfPar P, CdfTable* tab) {
   __shared__ CdfShared S;
   cdf_setup(P, S);
-  const int64_t i = (int64_t)blockIdx.x * kCdfBlock + threadIdx.x;
-  bool deferred = false;
-  if (i < n) {
-    const double xi = xs[i];
-    const CdfTrial T = cdf_prepare(fabs(xi), xi > 0, P, S);  // boundary, cdfdif_wrapper.pyx:46
-    double F = 0.0;
-    if (T.branch == 1) {
-      double h0 = 0, h1 = 0, h2 = 0;
-      bool conv = false;
-      for (int v = 0; v < kLaneTerms; ++v) {
-        h0 = h1;
-        h1 = h2;
-        h2 = h1 + beyond_term(v, T, P, S);
-        if (converged(h0, h1, h2)) {
-          conv = true;
-          break;
+  const int m = blockIdx.x, v = threadIdx.x;
+  if (m == 0) {
+    const double* src = (const double*)&S;
+    double* dst = (double*)&tab->S;
+    for (int k = v; k < (int)(sizeof(CdfShared) / sizeof(double)); k += 64) dst[k] = src[k];
+  }
+  if (v < kLaneTerms) {
+    const double a2 = P.a * P.a;
+    const double width = (P.Ter + (P.st / 2)) - (P.Ter - (P.st / 2));  // upper_t - lower_t
+    const double denom = beyond_denom(v, S.gk[m], a2);
+    const double dh = -.5 * denom;
+    tab->dh[m][v] = dh;
+    tab->lx[m][v] = beyond_lx(dh, width);
+    tab->fact[0][m][v] = beyond_fact(v, m, 0, denom, P, S);
+    tab->fact[1][m][v] = beyond_fact(v, m, 1, denom, P, S);
+  }
+}
+
+// Per-trial pass, G lanes per trial: trials below the window, and trials
+// beyond it whose series converges within kLaneTerms terms, are finished
+// here. Each step the G lanes of a trial evaluate G consecutive terms from the
+// LDS tables (one exp per drift node), then every lane of the group adds them
+// in v order with the reference's convergence test, so the partial sums —
+// and the stopping term — are the reference's (cdfdif.c:128-147). The rest —
+// window trials (36 series of up to 5000 terms each) and slowly converging
+// series near the window edge — are appended to `defer` for cdf_wave_kernel.
+template <int G>
+__global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, int64_t n,
+                                                             CdfPar P, const CdfTable* tab,
+                                                             double p_outlier, double w_outlier,
+                                                             double* out, int* defer,
+                                                             int* n_defer) {
+  static_assert(kLaneTerms % G == 0 && 64 % G == 0, "group size");
+  __shared__ CdfTable L;
+  {
+    const double* src = (const double*)tab;
+    double* dst = (double*)&L;
+    for (int k = threadIdx.x; k < (int)(sizeof(CdfTable) / sizeof(double)); k += kCdfBlock)
+      dst[k] = src[k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, j = lane % G, base = lane - j;
+  const int64_t per_block = kCdfBlock / G;
+  for (int64_t b = blockIdx.x; b * per_block < n; b += gridDim.x) {
+    const int64_t i = b * per_block + threadIdx.x / G;
+    const bool live = i < n;
+    const double xi = live ? xs[i] : 0.0;
+    const CdfTrial T = cdf_prepare(fabs(xi), xi > 0, P, L.S);  // boundary, cdfdif_wrapper.pyx:46
+    const double t_up = T.t - T.upper_t;
+    bool pend = live && T.branch == 1, conv = false;
+    double h0 = 0, h1 = 0, h2 = 0;
+    for (int v0 = 0; v0 < kLaneTerms && __ballot(pend); v0 += G) {
+      const int v = v0 + j;
+      double term = 0.0;
+      if (pend) {
+        double sum_nu = 0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+          sum_nu += L.fact[T.x][m][v] * exp((L.dh[m][v] * t_up) + L.lx[m][v]);
+        term = v * sum_nu;
+      }
+#pragma unroll
+      for (int k = 0; k < G; ++k) {
+        const double tk = G == 1 ? term : __shfl(term, base + k, 64);
+        if (pend) {
+          h0 = h1;
+          h1 = h2;
+          h2 = h1 + tk;
+          if (converged(h0, h1, h2)) {
+            pend = false;
+            conv = true;
+          }
         }
       }
-      if (conv) F = beyond_F(h2, T, P);
-      else deferred = true;
-    } else if (T.branch == 2) {
-      deferred = true;
     }
-    if (!deferred) out[i] = cdf_output(F, xi, p_outlier, w_outlier, S);
-  }
-  // wave-aggregated append (order irrelevant: outputs are per trial)
-  const unsigned long long b = __ballot(deferred);
-  if (b) {
-    const int lane = threadIdx.x & 63;
-    int base = 0;
-    if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
-    base = __shfl(base, 0, 64);
-    if (deferred) defer[base + __popcll(b & ((1ull << lane) - 1ull))] = (int)i;
+    const bool deferred = live && (T.branch == 2 || (T.branch == 1 && !conv));
+    if (live && !deferred && j == 0)
+      out[i] = cdf_output(T.branch == 1 ? beyond_F(h2, T, P) : 0.0, xi, p_outlier, w_outlier, L.S);
+    // wave-aggregated append (order irrelevant: outputs are per trial)
+    const bool app = deferred && j == 0;
+    const unsigned long long bal = __ballot(app);
+    if (bal) {
+      int at = 0;
+      if (lane == 0) at = atomicAdd(n_defer, __popcll(bal));
+      at = __shfl(at, 0, 64);
+      if (app) defer[at + __popcll(bal & ((1ull << lane) - 1ull))] = (int)i;
+    }
   }
 }
 
@@ -284,13 +369,20 @@ __global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, i
 // lanes 36+m the drift-node-~0 series, and sum_z / sum_nu are combined in the
 // reference's order.
 __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P,
-                                                     double p_outlier, double w_outlier,
-                                                     double* out, const int* defer,
-                                                     const int* n_defer) {
-  __shared__ CdfShared S;
-  cdf_setup(P, S);
-  const int lane = threadIdx.x;
+                                                     const CdfTable* tab, double p_outlier,
+                                                     double w_outlier, double* out,
+                                                     const int* defer, const int* n_defer) {
   const int nd = *n_defer;
+  if ((int)blockIdx.x >= nd) return;
+  __shared__ CdfShared S;
+  {
+    const double* src = (const double*)&tab->S;
+    double* dst = (double*)&S;
+    for (int k = threadIdx.x; k < (int)(sizeof(CdfShared) / sizeof(double)); k += 64)
+      dst[k] = src[k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x;
   for (int k = blockIdx.x; k < nd; k += gridDim.x) {
     const int idx = defer[k];
     const double xi = xs[idx];
@@ -341,11 +433,17 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
 }  // namespace
 
 // dmat_cdf_array on device x[n] (cdfdif_wrapper.pyx:16-53); *n_defer must be
-// 0 (the caller clears it on the stream). par holds the
-// wrapper's transformed parameters (a/10, t, sv/10+1e-10, z*a/10,
-// sz*a/10+1e-10, st+1e-10, v/10).
+// 0 (the caller clears it on the stream); tab holds kCdfTableDoubles doubles.
+// par holds the wrapper's transformed parameters (a/10, t, sv/10+1e-10,
+// z*a/10, sz*a/10+1e-10, st+1e-10, v/10).
+#ifndef WFPT_CDF_GROUP
+#define WFPT_CDF_GROUP 4
+#endif
+static_assert(sizeof(CdfTable) <= kCdfTableDoubles * sizeof(double), "kCdfTableDoubles");
+
 void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
-                     double w_outlier, double* out, int* defer, int* n_defer, hipStream_t s) {
+                     double w_outlier, double* out, double* tab, int* defer, int* n_defer,
+                     hipStream_t s) {
   if (n <= 0) return;
   CdfPar P;
   P.a = par[0];
@@ -355,13 +453,18 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   P.sZ = par[4];
   P.st = par[5];
   P.nu = par[6];
-  const int64_t nb = (n + kCdfBlock - 1) / kCdfBlock;
-  hipLaunchKernelGGL(dmat_cdf_kernel, dim3(nb), dim3(kCdfBlock), 0, s, x, n, P, p_outlier,
+  CdfTable* T = reinterpret_cast<CdfTable*>(tab);
+  hipLaunchKernelGGL(cdf_table_kernel, dim3(6), dim3(64), 0, s, P, T);
+  constexpr int G = WFPT_CDF_GROUP;
+  const int64_t per_block = kCdfBlock / G;
+  int64_t nb = (n + per_block - 1) / per_block;
+  if (nb > 8192) nb = 8192;
+  hipLaunchKernelGGL(dmat_cdf_kernel<G>, dim3(nb), dim3(kCdfBlock), 0, s, x, n, P, T, p_outlier,
                      w_outlier, out, defer, n_defer);
   // one wave per deferred trial on a fixed grid (it reads the count itself)
   const int64_t gw = n < 4096 ? n : 4096;
-  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, p_outlier, w_outlier, out,
-                     defer, n_defer);
+  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, T, p_outlier, w_outlier,
+                     out, defer, n_defer);
 }
 
 }  // namespace wfpt

@@ -144,6 +144,7 @@ struct wfpt_ctx {
   int* prof = nullptr;       // device: 16 refinement work counters (PROF_EVALS)
   unsigned long long* phase = nullptr;  // device: engine phase cycles (diagnostic builds)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
+  DevBuf<double> cdf_tab;    // dmat_cdf_array: the call's parameter-only tables
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
   DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
@@ -678,6 +679,7 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->prof) (void)hipFree(c->prof);
   if (c->phase) (void)hipFree(c->phase);
   c->defer.release();
+  c->cdf_tab.release();
   c->nd_idx.release();
   c->nd_par.release();
   c->nd_chunks.release();
@@ -1264,9 +1266,10 @@ int wfpt_dmat_cdf_array(wfpt_ctx* c, const double* x, int64_t n, const wfpt_para
   HIP_TRY(c->lp.reserve(n));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   HIP_TRY(c->defer.reserve(n + 1));
+  HIP_TRY(c->cdf_tab.reserve(wfpt::kCdfTableDoubles));
   HIP_TRY(hipMemsetAsync(c->defer.p + n, 0, sizeof(int), c->stream));
-  wfpt::launch_dmat_cdf(c->x.p, n, par, po, w_outlier, c->lp.p, c->defer.p, c->defer.p + n,
-                        c->stream);
+  wfpt::launch_dmat_cdf(c->x.p, n, par, po, w_outlier, c->lp.p, c->cdf_tab.p, c->defer.p,
+                        c->defer.p + n, c->stream);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   HIP_TRY(hipMemcpyAsync(out, c->lp.p, n * sizeof(double), hipMemcpyDeviceToHost, c->stream));

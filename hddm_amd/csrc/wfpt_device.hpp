@@ -135,6 +135,20 @@ constexpr double kDblMin = 2.2250738585072014e-308;
 // relative (checked against 120-bit arithmetic). 30 fp64 ops instead of OCML's
 // general-range sincospi (127). w == 1 is seeded with the reference's own
 // sin(fl(pi)) = 1.2246e-16 so the z = 1 edge keeps its nonzero value.
+// One Horner step of sincospi01: on the device a three-operand v_fma_f64 with
+// the coefficient in SGPRs (see horner below: fma() costs a v_mov_b64 per
+// step there), on the host fma() (the host builds the sine tables from the same
+// correctly rounded operations, so both produce the same bits).
+__host__ __device__ inline double horner_hd(double p, double r, double c) {
+#if defined(__HIP_DEVICE_COMPILE__) && (!defined(WFPT_HORNER_ASM) || WFPT_HORNER_ASM)
+  double d;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(p), "v"(r), "s"(c));
+  return d;
+#else
+  return fma(p, r, c);
+#endif
+}
+
 __host__ __device__ inline void sincospi01(double w, double& s, double& c) {
   const double t = 2.0 * w;
   const double n = rint(t);
@@ -142,22 +156,22 @@ __host__ __device__ inline void sincospi01(double w, double& s, double& c) {
   const double x = f * 1.5707963267948966;  // pi/2
   const double x2 = x * x;
   double ps = 0x1.952c77030ad4ap-49;
-  ps = fma(ps, x2, -0x1.ae7f3e733b81fp-41);
-  ps = fma(ps, x2, 0x1.6124613a86d09p-33);
-  ps = fma(ps, x2, -0x1.ae64567f544e4p-26);
-  ps = fma(ps, x2, 0x1.71de3a556c734p-19);
-  ps = fma(ps, x2, -0x1.a01a01a01a01ap-13);
-  ps = fma(ps, x2, 0x1.1111111111111p-7);
-  ps = fma(ps, x2, -0x1.5555555555555p-3);
+  ps = horner_hd(ps, x2, -0x1.ae7f3e733b81fp-41);
+  ps = horner_hd(ps, x2, 0x1.6124613a86d09p-33);
+  ps = horner_hd(ps, x2, -0x1.ae64567f544e4p-26);
+  ps = horner_hd(ps, x2, 0x1.71de3a556c734p-19);
+  ps = horner_hd(ps, x2, -0x1.a01a01a01a01ap-13);
+  ps = horner_hd(ps, x2, 0x1.1111111111111p-7);
+  ps = horner_hd(ps, x2, -0x1.5555555555555p-3);
   const double sx = fma(x * x2, ps, x);
   double pc = -0x1.6827863b97d97p-53;
-  pc = fma(pc, x2, 0x1.ae7f3e733b81fp-45);
-  pc = fma(pc, x2, -0x1.93974a8c07c9dp-37);
-  pc = fma(pc, x2, 0x1.1eed8eff8d898p-29);
-  pc = fma(pc, x2, -0x1.27e4fb7789f5cp-22);
-  pc = fma(pc, x2, 0x1.a01a01a01a01ap-16);
-  pc = fma(pc, x2, -0x1.6c16c16c16c17p-10);
-  pc = fma(pc, x2, 0x1.5555555555555p-5);
+  pc = horner_hd(pc, x2, 0x1.ae7f3e733b81fp-45);
+  pc = horner_hd(pc, x2, -0x1.93974a8c07c9dp-37);
+  pc = horner_hd(pc, x2, 0x1.1eed8eff8d898p-29);
+  pc = horner_hd(pc, x2, -0x1.27e4fb7789f5cp-22);
+  pc = horner_hd(pc, x2, 0x1.a01a01a01a01ap-16);
+  pc = horner_hd(pc, x2, -0x1.6c16c16c16c17p-10);
+  pc = horner_hd(pc, x2, 0x1.5555555555555p-5);
   const double cx = fma(x2 * x2, pc, fma(-0.5, x2, 1.0));
   const bool q1 = n == 1.0, q2 = n == 2.0;
   s = q1 ? cx : (q2 ? -sx : sx);
@@ -1048,6 +1062,49 @@ __device__ inline void put5(double (&v)[5], int i, double x) {
 // overflow): libm's exp, which gives 0 for -inf like the reference
 // (exp_val's range reduction would make NaN of it).
 __device__ inline double exp_sat(double x) { return exp(x); }
+
+// log of a trial's density term (wfpt.pyx:44, :70 — every per-trial log the
+// kernels emit). Values only: the published fdlibm reduction x = 2^k (1 + f),
+// sqrt(2)/2 <= 1 + f < sqrt(2), s = f / (2 + f) (hardware reciprocal + two
+// Newton steps + one residual correction), log(1 + f) = f - (hfsq - s (hfsq +
+// R(s^2))) with fdlibm's degree-7 R, plus k ln2 in two parts. <= 0.81 ulp
+// (2e7 random arguments incl. subnormals against long double, unbiased), 38
+// VALU operations against OCML's double-double log (~98). Zero, negative,
+// infinite and NaN arguments take OCML's log. WFPT_FAST_LOG=0: OCML's log.
+#ifndef WFPT_FAST_LOG
+#define WFPT_FAST_LOG 1
+#endif
+__device__ inline double log_val(double x) {
+#if WFPT_FAST_LOG
+  if (!(x > 0.0 && x < __builtin_inf())) return log(x);
+  int e;
+  double m = frexp(x, &e);
+  if (m < 0.70710678118654752440) {
+    m = m + m;
+    e -= 1;
+  }
+  const double f = m - 1.0;
+  const double d = 2.0 + f;
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  r = fma(r, fma(-d, r, 1.0), r);
+  double sq = f * r;
+  sq = fma(r, fma(-d, sq, f), sq);
+  const double z = sq * sq, w = z * z;
+  const double t1 = w * horner(fma(w, 1.531383769920937332e-01, 2.222219843214978396e-01), w,
+                               3.999999999940941908e-01);
+  const double t2 = z * horner(horner(fma(w, 1.479819860511658591e-01, 1.818357216161805012e-01),
+                                      w, 2.857142874366239149e-01),
+                               w, 6.666666666666735130e-01);
+  const double R = t2 + t1;
+  const double hfsq = (0.5 * f) * f;
+  const double k = (double)e;
+  return k * 6.93147180369123816490e-01 -
+         ((hfsq - fma(sq, hfsq + R, k * 1.90821492927058770002e-10)) - f);
+#else
+  return log(x);
+#endif
+}
 
 __device__ inline double exp_node(double x) {
 #if WFPT_FAST_EXP && WFPT_NODE_FAST_EXP

@@ -129,11 +129,11 @@ template <int OUT>
 __device__ inline void emit(const TrialArgs& A, int64_t i, double p, double& lp, int& zero) {
   if (OUT == OUT_ARRAY) {
     p = p * (1 - A.P.p_outlier) + (A.K.w_outlier * A.P.p_outlier);  // wfpt.pyx:44
-    A.out[i] = A.logp ? log(p) : p;
+    A.out[i] = A.logp ? log_val(p) : p;
   } else {
     p = p * (1 - A.P.p_outlier) + A.wp_outlier;  // wfpt.pyx:70
     if (p == 0) zero = 1;
-    else lp = log(p);
+    else lp = log_val(p);
     if (OUT == OUT_LOGP) A.out[i] = zero ? -INFINITY : lp;
     if (OUT == OUT_BOTH) A.trial[i] = zero ? -INFINITY : lp;
   }
@@ -896,7 +896,7 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
 __device__ inline double node_logp(double p, const Params& Q, const Knobs& K) {
   const bool ok = (Q.p_outlier >= 0) & (Q.p_outlier <= 1);  // wfpt.pyx:63-64 per node
   p = p * (1 - Q.p_outlier) + K.w_outlier * Q.p_outlier;
-  return (!ok || p == 0) ? -INFINITY : log(p);
+  return (!ok || p == 0) ? -INFINITY : log_val(p);
 }
 
 // The per-call tables (EngTables) of one trial's parameters, built by the lanes
@@ -983,7 +983,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
                               : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
       }
       ne += n1;
-      lp[i] = MULTI ? log(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier))
+      lp[i] = MULTI ? log_val(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier))
                     : node_logp(p, Q, K);
     }
     wave_sync();  // the next record reuses this wave's LDS
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(
     flags |= f1 & kFlagErrors;
     p = settle(p, x[i], Q, K, false, n1, flags);
     ne += n1;
-    lp[i] = MULTI ? log(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier)) : node_logp(p, Q, K);
+    lp[i] = MULTI ? log_val(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier)) : node_logp(p, Q, K);
   }
   if (flags & kFlagErrors) atomicOr(status, flags & kFlagErrors);
   if (COUNT) {
@@ -1751,7 +1751,7 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(
       p = 1 - prob_ub(Q.v, Q.a, Q.z);
     }
     // the reference has no early exit here: log(0) = -inf enters the sum
-    lp = log(p);
+    lp = log_val(p);
     if (lpo) lpo[i] = lp;
   }
   block_reduce<false>(lp, zero, ne);
@@ -1805,11 +1805,11 @@ void multi_fast_kernel(const double* x, int64_t n, const double* const* arr, con
       int flags = 0;
       unsigned pend;
       const int oc = fast_level0<MODE>(xi, Q, K, p, f, ne, flags, pend);
-      if (oc == kFinal) lp[i] = log(p * (1 - p_outlier) + (K.w_outlier * p_outlier));
+      if (oc == kFinal) lp[i] = log_val(p * (1 - p_outlier) + (K.w_outlier * p_outlier));
       else defer = true;
     } else {
       const double pu = prob_ub(Q.v, Q.a, Q.z);
-      lp[i] = log(xi == 999. ? pu : 1 - pu);
+      lp[i] = log_val(xi == 999. ? pu : 1 - pu);
     }
   }
   const unsigned long long b = __ballot(defer);

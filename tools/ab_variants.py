@@ -82,8 +82,12 @@ def run(reps, names=None):
     out = {k: [] for k in names}
     for r in range(reps):
         for name in names:
-            env = dict(os.environ, WFPT_AMD_LIB=os.path.join(LIBDIR, f"libwfpt_{name}.so"),
-                       ROOT=ROOT)
+            lib = os.path.join(LIBDIR, f"libwfpt_{name}.so")
+            if not os.path.exists(lib):  # hddm_amd.build variants: lib_<name>.so
+                lib = os.path.join(LIBDIR, f"lib_{name}.so")
+            if name == "default" and not os.path.exists(lib):
+                lib = os.path.join(ROOT, "hddm_amd", "lib", "libwfpt_amd.so")
+            env = dict(os.environ, WFPT_AMD_LIB=lib, ROOT=ROOT)
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True,
                                text=True, timeout=600)
             line = [l for l in p.stdout.splitlines() if l.startswith("RESULT ")]

@@ -41,6 +41,9 @@ def main():
     ap.add_argument("tag")
     ap.add_argument("--kernel", default="void wfpt::lean_kernel<3, false, 0>")
     ap.add_argument("--trials", type=int, default=1_000_000)
+    ap.add_argument("--bytes-per-trial", type=float, default=8.0,
+                    help="algorithmic HBM bytes per trial: 8 for the summing kernels (rt in, "
+                         "a sum out), 16 for per-trial outputs (x in, value out)")
     ap.add_argument("--prof-dir", default=PROF, help="tools/gpu_profile*.sh output directory")
     ap.add_argument("--name", default="pmc_summary", help="summary file name under profiles/<tag>/")
     ap.add_argument("--no-traffic", action="store_true",
@@ -72,7 +75,7 @@ def main():
         "counters_per_launch": res,
         "hbm_read_bytes": fetch_b, "hbm_write_bytes": write_b,
         "hbm_bytes_per_launch": fetch_b + write_b,
-        "algorithmic_bytes_per_launch": 8.0 * a.trials,
+        "algorithmic_bytes_per_launch": a.bytes_per_trial * a.trials,
         "valu_lane_ops_per_trial": valu * 64 / a.trials,
         "fp64_lane_ops_per_trial": f64 * 64 / a.trials,
         "fp64_lane_ops_per_s": f64 * 64 / t,
