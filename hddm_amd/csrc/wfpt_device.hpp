@@ -1639,8 +1639,8 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
   const double ia2 = 1.0 / a2;
   H.ia2 = ia2;
   // values only (the fp32 decision estimates below have a 1e-5 guard band)
-  const double q0 = exp((-kPi2 * ((x - lb) * ia2)) * 0.5);
-  const double R = exp((kPi2 * (ub - lb)) * (0.125 * ia2));
+  const double q0 = exp_node((-kPi2 * ((x - lb) * ia2)) * 0.5);
+  const double R = exp_node((kPi2 * (ub - lb)) * (0.125 * ia2));
   if (q0 > 1e-280 && R < 1e10 && x - lb > 0) {
     H.q0 = q0;
     H.R = R;

@@ -240,10 +240,12 @@ constexpr int kQCap = 2 * (1 << kTreeDepth) * 64;  // tasks (or z walks) of one 
 constexpr int kFlagIdle = 16;                       // lane without a trial to integrate
 constexpr int kFlagStop = kFlagExact | kFlagFallback | kFlagIdle;
 
-// WFPT_ZWALK_LDS: a z walk's 17 values are staged in LDS (ZV) for the lane
-// that runs its tree17; 0: gathered by wave shuffles (no LDS, no barrier)
+// WFPT_ZWALK_LDS=1: a z walk's 17 values are staged in LDS (ZV) for the lane
+// that runs its tree17; 0 (default): gathered by wave shuffles (no LDS, no
+// barrier; 3-4% faster on the stress sets in the r04 interleaved A/B despite
+// 28 B of engine scratch)
 #ifndef WFPT_ZWALK_LDS
-#define WFPT_ZWALK_LDS 1
+#define WFPT_ZWALK_LDS 0
 #endif
 // LDS of one chunk under refinement by a team of TW waves.
 template <int TW>
