@@ -198,25 +198,53 @@ __device__ inline double beyond_F(double h2, const CdfTrial& T, const CdfPar& P)
 }
 
 // Window branch, drift node m with |gk| > eps, start-point node i: the
-// increment of sum_z (cdfdif.c:161-182).
+// increment of sum_z (cdfdif.c:161-182). Term v of its series is
+// (v sin(sifa zzz)) exp(-denom/2 (t - lower_t) - 2 log(denom)), where only
+// t - lower_t depends on the trial: for v < kWinTerms the other factors come
+// from the per-call table (window_terms, the same operations), past it they
+// are computed here.
+constexpr int kWinTerms = 512;
+struct CdfWinTable {
+  double vs[kWinTerms][2][6];  // v sin(sifa zzz(x, i))
+  double dh[kWinTerms][6];     // -denom(v, m) / 2
+  double l2[kWinTerms][6];     // 2 log(denom(v, m))
+};
+
+__device__ inline double window_zzz(int x, int i, const CdfPar& P, const CdfShared& S) {
+  const double gzi = S.gz[i];
+  return ((P.a - gzi) * x) + (gzi * (1 - x));
+}
+__device__ inline double window_denom(int v, double g, double a2) {
+  return ((g * g) * 100) + (((kCPi * v) * (kCPi * v)) / (a2 * 100));
+}
+__device__ inline double window_vs(int v, double zzz, double a) {
+  const double sifa = (kCPi * v) / a;
+  return v * sin(sifa * zzz);
+}
+
 __device__ inline double window_mi(int m, int i, const CdfTrial& T, const CdfPar& P,
-                                   const CdfShared& S) {
+                                   const CdfShared& S, const CdfWinTable* __restrict__ W) {
   const double a = P.a, a2 = a * a, st = P.st, t = T.t, lower_t = T.lower_t;
   const int x = T.x, sg = T.sg, sh = T.sh;
   const double g = S.gk[m];
   const double B = ((sh * g) * kCPi) * .01;
   const double sD = sinh(((sh * g) * a) / .01);
-  const double gzi = S.gz[i];
-  const double zzz = ((a - gzi) * x) + (gzi * (1 - x));
+  const double zzz = window_zzz(x, i, P, S);
   const double ser = (((-((a * a2) / B)) * sinh(((zzz * sh) * g) / .01)) / (sD * sD)) +
                      ((((zzz * a2) / B) * cosh((((a - zzz) * sh) * g) / .01)) / sD);
+  const double tl = t - lower_t;
   double h0 = 0, h1 = 0, h2 = 0;
   for (int v = 0; v < kVMax; ++v) {
     h0 = h1;
     h1 = h2;
-    const double sifa = (kCPi * v) / a;
-    const double denom = ((g * g) * 100) + (((kCPi * v) * (kCPi * v)) / (a2 * 100));
-    h2 = h1 + ((v * sin(sifa * zzz)) * exp(((-.5 * denom) * (t - lower_t)) - (2 * log(denom))));
+    double term;
+    if (v < kWinTerms) {
+      term = W->vs[v][x][i] * exp((W->dh[v][m] * tl) - W->l2[v][m]);
+    } else {
+      const double denom = window_denom(v, g, a2);
+      term = window_vs(v, zzz, a) * exp(((-.5 * denom) * tl) - (2 * log(denom)));
+    }
+    h2 = h1 + term;
     if (converged(h0, h1, h2)) break;
   }
   return ((((.5 * S.w_g[i]) * (ser - (4 * h2))) * (kCPi / 100)) / (a2 * st)) *
@@ -269,9 +297,25 @@ struct CdfTable {
 
 // One block per drift node m, one lane per v: the parameter-only state
 // (cdf_setup) and the (v, m) factors of the beyond-window series.
-__global__ __launch_bounds__(64) void cdf_table_kernel(CdfPar P, CdfTable* tab) {
+constexpr int kWinVsBlocks = kWinTerms * 12 / 64, kWinDenBlocks = kWinTerms * 6 / 64;
+constexpr int kCdfTableBlocks = 6 + kWinVsBlocks + kWinDenBlocks;
+__global__ __launch_bounds__(64) void cdf_table_kernel(CdfPar P, CdfTable* tab, CdfWinTable* W) {
   __shared__ CdfShared S;
   cdf_setup(P, S);
+  if (blockIdx.x >= 6) {  // the window series' tables
+    const double a2 = P.a * P.a;
+    const int b = blockIdx.x - 6;
+    if (b < kWinVsBlocks) {
+      const int e = b * 64 + threadIdx.x, v = e / 12, x = (e % 12) / 6, i = e % 6;
+      W->vs[v][x][i] = window_vs(v, window_zzz(x, i, P, S), P.a);
+    } else {
+      const int e = (b - kWinVsBlocks) * 64 + threadIdx.x, v = e / 6, m = e % 6;
+      const double denom = window_denom(v, S.gk[m], a2);
+      W->dh[v][m] = -.5 * denom;
+      W->l2[v][m] = 2 * log(denom);
+    }
+    return;
+  }
   const int m = blockIdx.x, v = threadIdx.x;
   if (m == 0) {
     const double* src = (const double*)&S;
@@ -369,7 +413,9 @@ __global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, i
 // lanes 36+m the drift-node-~0 series, and sum_z / sum_nu are combined in the
 // reference's order.
 __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P,
-                                                     const CdfTable* tab, double p_outlier,
+                                                     const CdfTable* tab,
+                                                     const CdfWinTable* __restrict__ W,
+                                                     double p_outlier,
                                                      double w_outlier, double* out,
                                                      const int* defer, const int* n_defer) {
   const int nd = *n_defer;
@@ -410,7 +456,7 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
       double val = 0.0;
       if (lane < 36) {
         const int m = lane / 6, i = lane % 6;
-        if (fabs(S.gk[m]) > kEps) val = window_mi(m, i, T, P, S);
+        if (fabs(S.gk[m]) > kEps) val = window_mi(m, i, T, P, S, W);
       } else if (lane < 42) {
         if (!(fabs(S.gk[lane - 36]) > kEps)) val = window_m0(T, P);
       }
@@ -433,13 +479,18 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
 }  // namespace
 
 // dmat_cdf_array on device x[n] (cdfdif_wrapper.pyx:16-53); *n_defer must be
-// 0 (the caller clears it on the stream); tab holds kCdfTableDoubles doubles.
+// 0 (the caller clears it on the stream); tab holds kCdfTableDoubles doubles
+// (the per-call tables).
 // par holds the wrapper's transformed parameters (a/10, t, sv/10+1e-10,
 // z*a/10, sz*a/10+1e-10, st+1e-10, v/10).
 #ifndef WFPT_CDF_GROUP
 #define WFPT_CDF_GROUP 4
 #endif
-static_assert(sizeof(CdfTable) <= kCdfTableDoubles * sizeof(double), "kCdfTableDoubles");
+// the buffer: CdfTable, then CdfWinTable at kCdfTableBeyond doubles
+constexpr int kCdfTableBeyond = 1344;
+static_assert(sizeof(CdfTable) <= kCdfTableBeyond * sizeof(double), "kCdfTableBeyond");
+static_assert(kCdfTableBeyond * sizeof(double) + sizeof(CdfWinTable) <=
+                  kCdfTableDoubles * sizeof(double), "kCdfTableDoubles");
 
 void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
                      double w_outlier, double* out, double* tab, int* defer, int* n_defer,
@@ -454,7 +505,8 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   P.st = par[5];
   P.nu = par[6];
   CdfTable* T = reinterpret_cast<CdfTable*>(tab);
-  hipLaunchKernelGGL(cdf_table_kernel, dim3(6), dim3(64), 0, s, P, T);
+  CdfWinTable* W = reinterpret_cast<CdfWinTable*>(tab + kCdfTableBeyond);
+  hipLaunchKernelGGL(cdf_table_kernel, dim3(kCdfTableBlocks), dim3(64), 0, s, P, T, W);
   constexpr int G = WFPT_CDF_GROUP;
   const int64_t per_block = kCdfBlock / G;
   int64_t nb = (n + per_block - 1) / per_block;
@@ -463,7 +515,7 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
                      w_outlier, out, defer, n_defer);
   // one wave per deferred trial on a fixed grid (it reads the count itself)
   const int64_t gw = n < 4096 ? n : 4096;
-  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, T, p_outlier, w_outlier,
+  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, T, W, p_outlier, w_outlier,
                      out, defer, n_defer);
 }
 
