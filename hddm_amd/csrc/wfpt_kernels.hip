@@ -365,7 +365,10 @@ __device__ inline void refine_rounds(const TrialArgs& A, ChunkLds<TW>& cl, int t
     if (stage == 1 && (MODE != kAdaptTZ || r * 16 * TW >= nz)) stage = 2;
     if (stage == 2) {
       pc.mark(2);
-      if (L <= 2) ty.z[L] = nz;
+      // constant indices: a runtime index would put the tally in scratch
+      if (L == 0) ty.z[0] = nz;
+      else if (L == 1) ty.z[1] = nz;
+      else if (L == 2) ty.z[2] = nz;
       // stop tests of level L, each owner lane its own tree
       unsigned need = 0u;
       if (tid < 64 && !(cl.fl[tid] & kFlagStop)) {
