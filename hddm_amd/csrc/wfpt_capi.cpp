@@ -148,7 +148,8 @@ struct wfpt_ctx {
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
   DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
-  int* n_defer = nullptr;    // device [2]: deferred counts of the per-node fast path (0 at rest)
+  int* n_defer = nullptr;    // device [4]: the per-node path's listed chunks, chunk-path records,
+                             // fast-pass records (0 at rest)
   unsigned long long* evals = nullptr;
   int* status = nullptr;      // device: Simpson-stack overflow flag
   int* host_status = nullptr; // pinned mirror
@@ -631,8 +632,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
     e = hipHostMalloc((void**)&c->mres, 8 * sizeof(double),
                       hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, 2 * sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->n_defer, 0, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, 4 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->n_defer, 0, 4 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
@@ -1008,7 +1009,7 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
     HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>((d->n + 63) / 64, 1)));
-    HIP_TRY(hipMemsetAsync(c->n_defer, 0, 2 * sizeof(int), c->stream));
+    HIP_TRY(hipMemsetAsync(c->n_defer, 0, 3 * sizeof(int), c->stream));
   }
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));

@@ -310,6 +310,19 @@ __device__ inline void load_tree(const ChunkLds<TW>& cl, int o, double (&f)[kTre
 }
 
 // Work tallies of one chunk (COUNT builds; wfpt_profile_lists).
+// Per-node path: deferred trials run as records (one wave per trial,
+// node_engine_kernel) when they average at most kNodeRecPerChunk per listed
+// chunk, else 64 trials per wave through their chunks (node_chunk_kernel),
+// which re-runs every trial of a chunk. Both produce each trial's term with
+// the same operations; the choice depends only on the call's inputs.
+#ifndef WFPT_NODE_REC_PER_CHUNK
+#define WFPT_NODE_REC_PER_CHUNK 8
+#endif
+constexpr int kNodeRecPerChunk = WFPT_NODE_REC_PER_CHUNK;
+__device__ inline bool node_records_sparse(int n_records, int n_chunks) {
+  return (long long)n_records <= (long long)kNodeRecPerChunk * n_chunks;
+}
+
 struct Tally {
   int t1 = 0, t2 = 0, rec = 0, z[3] = {0, 0, 0};
 };
@@ -940,11 +953,15 @@ __device__ inline void eng_tables_wave(const Params& P, EngTables& T, int lane) 
 template <int MODE, bool COUNT, bool MULTI>
 __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
     const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
-    const int* n_defer, unsigned long long* evals, int* status) {
+    const int* n_defer, unsigned long long* evals, int* status,
+    const int* n_chunks = nullptr) {
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
   const int nd = *n_defer;
+  // per-node path: the records run here only when they are sparse in their
+  // chunks (node_records_sparse); node_chunk_kernel completes them otherwise
+  if (n_chunks && !node_records_sparse(nd, *n_chunks)) return;
   const int nwaves = (int)gridDim.x * kEngWaves;
   long long ne = 0;
   int errf = 0;
@@ -1520,8 +1537,20 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
         d_idx[k] = i;
         d_par[k] = Q;
       }
-    } else if (lane == 0) {
-      clist[atomicAdd(n_chunks, 1)] = (int)(i >> 6);
+    } else {
+      // the chunk for node_chunk_kernel and the trials as records for
+      // node_engine_kernel (fast-pass records counted in n_chunks[2])
+      int base = 0;
+      if (lane == 0) {
+        clist[atomicAdd(n_chunks, 1)] = (int)(i >> 6);
+        base = atomicAdd(n_chunks + 2, __popcll(b));
+      }
+      base = __shfl(base, 0, 64);
+      if (defer) {
+        const int k = base + __popcll(b & lanemask_lt(lane));
+        d_idx[k] = i;
+        d_par[k] = Q;
+      }
     }
   }
   if (COUNT) {
@@ -1558,6 +1587,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
   const int nc = *n_chunks;
+  if (node_records_sparse(n_chunks[2], nc)) return;  // node_engine_kernel runs the records
   const int nwaves = (int)gridDim.x * kEngWaves;
   long long ne = 0;
   int nseg = 0, nex = 0, nwk = 0;
@@ -1640,7 +1670,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
         }
       }
       if (mine && !defer) {
-        ne += n1;
+        if (oc != kFinal) ne += n1;  // node_fast_kernel counted the trials it settled
         lp[i] = node_logp(p, Q, K);
       }
       wave_sync();  // the next segment rebuilds this wave's LDS
@@ -2037,8 +2067,14 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                      node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
                      prof);
   if constexpr (MODE != kDirect) {
-    // adaptive families: one wave per listed chunk (node_chunk_kernel)
+    // adaptive families: the fast pass's records, one wave each, when they
+    // are sparse in their chunks (node_engine_kernel), else one wave per
+    // listed chunk (node_chunk_kernel, whose exact / walk records reuse the
+    // record buffers); each kernel reads the counts and runs only when chosen
     const int64_t nw = (n + 63) / 64;
+    const int64_t nr = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 1024);
+    hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, false>), dim3(nr), dim3(kEngBlock), 0, s,
+                       x, K, lp, d_idx, d_par, n_defer + 2, evals, status, n_defer);
     const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
                        n, P, K, lp, clist, n_defer, d_idx, d_par, n_defer + 1, evals, prof);
