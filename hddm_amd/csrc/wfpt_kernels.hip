@@ -2072,19 +2072,21 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     // listed chunk (node_chunk_kernel, whose exact / walk records reuse the
     // record buffers); each kernel reads the counts and runs only when chosen
     const int64_t nw = (n + 63) / 64;
-    const int64_t nr = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 1024);
+    // grids of the kernels that usually exit at once stay small: their waves
+    // carry kilobytes of scratch per lane (the exact path on one lane)
+    const int64_t nr = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 256);
     hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, false>), dim3(nr), dim3(kEngBlock), 0, s,
                        x, K, lp, d_idx, d_par, n_defer + 2, evals, status, n_defer);
     const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
                        n, P, K, lp, clist, n_defer, d_idx, d_par, n_defer + 1, evals, prof);
-    const int64_t g = std::min<int64_t>(nw, 2048);
+    const int64_t g = std::min<int64_t>(nw, 64);
     hipLaunchKernelGGL((node_defer_kernel<MODE, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp, d_idx,
                        d_par, n_defer + 1, evals, status);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;
-    const int64_t g = nl < 2048 ? nl : 2048;
+    const int64_t g = nl < 64 ? nl : 64;  // rare exact-path records; kilobytes of scratch per lane
     hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
                        d_idx, d_par, n_defer, evals, status);
   }
@@ -2174,13 +2176,13 @@ static void launch_multi_two_pass(const double* x, int64_t n, const double* cons
                      n, arr, scal, K, p_outlier, lp, d_idx, d_par, n_defer, evals);
   if constexpr (MODE != kDirect) {
     // adaptive families: one wave per deferred record (node_engine_kernel)
-    const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 1024);
+    const int64_t nb = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 256);
     hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, true>), dim3(nb), dim3(kEngBlock), 0, s, x,
                        K, lp, d_idx, d_par, n_defer, evals, status);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;
-    const int64_t g = nl < 2048 ? nl : 2048;
+    const int64_t g = nl < 64 ? nl : 64;  // rare exact-path records; kilobytes of scratch per lane
     hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT, true>), dim3(g), dim3(64), 0, s, x, K, lp,
                        d_idx, d_par, n_defer, evals, status);
   }
