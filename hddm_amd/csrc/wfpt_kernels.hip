@@ -23,9 +23,9 @@
 // (wfpt_wiener_like_trials: the per-trial check of the summing path).
 // Fixed Simpson (use_adaptive = 0): trial_kernel. Per-node parameters
 // (wfpt_wiener_like_nodes): node_fast_kernel (level 0, LDS-staged node rows)
-// + node_chunk_kernel (listed chunks, 64 trials per wave per node segment) +
-// node_defer_kernel (exact / walk records); generic node_kernel for mixed
-// families. Per-trial parameters (wiener_like_multi): multi_fast_kernel +
+// + node_chunk_kernel (the deferred trials one wave each when they are sparse
+// in their chunks, else the listed chunks 64 trials per wave per node
+// segment); generic node_kernel for mixed families. Per-trial parameters (wiener_like_multi): multi_fast_kernel +
 // node_engine_kernel<..., MULTI> (one wave per deferred record), or the
 // generic multi_kernel.
 #include "wfpt_device.hpp"
@@ -950,23 +950,17 @@ __device__ inline void eng_tables_wave(const Params& P, EngTables& T, int lane) 
 // levels and z walks across the lanes, exactly as a split unit of the dataset
 // engine. Trees deeper than kTreeDepth and rounding-critical values take the
 // per-lane fallback / exact path on lane 0. MULTI: wiener_like_multi's term.
+// One wave per record, wave ids w0, w0 + nwaves, ...: the record's tables in
+// the wave's LDS, its level-0 t nodes as tasks, the refinement rounds, and on
+// lane 0 its density (tree17, the exact path or the per-lane walk) and term.
 template <int MODE, bool COUNT, bool MULTI>
-__global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
-    const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
-    const int* n_defer, unsigned long long* evals, int* status,
-    const int* n_chunks = nullptr) {
-  __shared__ ChunkLds<1> lds[kEngWaves];
-  const int lane = threadIdx.x & 63;
-  ChunkLds<1>& cl = lds[threadIdx.x >> 6];
-  const int nd = *n_defer;
-  // per-node path: the records run here only when they are sparse in their
-  // chunks (node_records_sparse); node_chunk_kernel completes them otherwise
-  if (n_chunks && !node_records_sparse(nd, *n_chunks)) return;
-  const int nwaves = (int)gridDim.x * kEngWaves;
+__device__ inline void node_records(ChunkLds<1>& cl, int lane, int w0, int nwaves,
+                                    const double* x, const Knobs& K, double* lp,
+                                    const int64_t* d_idx, const Params* d_par, int nd,
+                                    unsigned long long* evals, int* status) {
   long long ne = 0;
   int errf = 0;
-  for (int k = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
-       k < nd; k += nwaves) {
+  for (int k = w0; k < nd; k += nwaves) {
     const int64_t i = d_idx[k];
     const Params Q = d_par[k];
     TrialArgs A{};
@@ -1015,6 +1009,18 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
     ne = wave_sum_ll(ne);
     if (lane == 0) atomicAdd(evals, (unsigned long long)ne);
   }
+}
+
+template <int MODE, bool COUNT, bool MULTI>
+__global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
+    const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
+    const int* n_defer, unsigned long long* evals, int* status) {
+  __shared__ ChunkLds<1> lds[kEngWaves];
+  const int lane = threadIdx.x & 63;
+  node_records<MODE, COUNT, MULTI>(
+      lds[threadIdx.x >> 6], lane,
+      __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6)),
+      (int)gridDim.x * kEngWaves, x, K, lp, d_idx, d_par, *n_defer, evals, status);
 }
 
 // Folds every chunk's deferred trials into it, one wave per chunk: slot k of
@@ -1573,27 +1579,33 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
 // per-lane walk for the rare trials the rounds hand on) and its term. Every
 // trial of a listed chunk is rewritten (the same level-0 operations as the
 // fast pass), so a chunk's terms do not depend on which lanes deferred.
-// Replaces one wave per deferred trial: a call where most trials refine (an
-// MCMC proposal far in the tails) runs 64 trials per wave.
-// Trials the rounds hand on (the exact path, trees deeper than kTreeDepth)
-// become (2 i + exact, parameter row) records for node_defer_kernel (one lane
-// each), so this kernel carries neither path's registers nor stack.
+// A call where most trials refine (an MCMC proposal far in the tails) runs
+// 64 trials per wave this way; when the deferred trials are sparse in their
+// chunks (node_records_sparse: the usual MCMC call) the same launch runs the
+// fast pass's records one wave each instead (node_records), which skips the
+// level 0 of the chunks' settled trials. Trials the rounds hand on (the exact
+// path, trees deeper than kTreeDepth) are settled on their own lane (rare).
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
-    const int* clist, const int* n_chunks, int64_t* d_rec, Params* d_par, int* n_rec,
-    unsigned long long* evals, int* prof) {
+    const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
+    unsigned long long* evals, int* status, int* prof) {
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
-  const int nc = *n_chunks;
-  if (node_records_sparse(n_chunks[2], nc)) return;  // node_engine_kernel runs the records
+  const int nc = n_chunks[0], nrec = n_chunks[2];
   const int nwaves = (int)gridDim.x * kEngWaves;
+  const int w0 =
+      __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
+  if (node_records_sparse(nrec, nc)) {  // a few deferred trials: one wave each
+    node_records<MODE, COUNT, false>(cl, lane, w0, nwaves, x, K, lp, r_idx, r_par, nrec, evals,
+                                     status);
+    return;
+  }
   long long ne = 0;
-  int nseg = 0, nex = 0, nwk = 0;
+  int nseg = 0, nex = 0, nwk = 0, errf = 0;
   Tally ty;
-  for (int k = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
-       k < nc; k += nwaves) {
+  for (int k = w0; k < nc; k += nwaves) {
     const int64_t c = clist[k];
     const int64_t i = c * 64 + lane;
     const bool own = i < n;
@@ -1657,25 +1669,20 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
         tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
         if (COUNT) n1 = cl.cnt[lane];
       }
-      const unsigned long long db = __ballot(defer);
-      if (db) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(n_rec, __popcll(db));
-        base = __shfl(base, 0, 64);
-        if (defer) {
-          const int r = base + __popcll(db & lanemask_lt(lane));
-          d_rec[r] = 2 * i + ((rf & kFlagExact) ? 1 : 0);
-          d_par[r] = Q;
-          if (COUNT) ++((rf & kFlagExact) ? nex : nwk);
-        }
+      if (defer) {  // rare: the exact path or the per-lane walk, on this lane
+        n1 = 0;
+        p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
+                              : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+        if (COUNT) ++((rf & kFlagExact) ? nex : nwk);
       }
-      if (mine && !defer) {
+      if (mine) {
         if (oc != kFinal) ne += n1;  // node_fast_kernel counted the trials it settled
         lp[i] = node_logp(p, Q, K);
       }
       wave_sync();  // the next segment rebuilds this wave's LDS
     }
   }
+  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
   if (COUNT) {
     ne = wave_sum_ll(ne);
     nex = (int)wave_sum_ll(nex);
@@ -1693,31 +1700,6 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
       atomicAdd(&prof[9], ty.z[1]);
       atomicAdd(&prof[10], ty.z[2]);
     }
-  }
-}
-
-// The records node_chunk_kernel handed on, one lane each: the exact path or
-// the per-lane walk (fold_kernel's operations), then the node's term.
-template <int MODE, bool COUNT>
-__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_defer_kernel(
-    const double* x, Knobs K, double* lp, const int64_t* d_rec, const Params* d_par,
-    const int* n_rec, unsigned long long* evals, int* status) {
-  const int nd = *n_rec;
-  long long ne = 0;
-  int errf = 0;
-  for (int64_t k = (int64_t)blockIdx.x * 64 + threadIdx.x; k < nd; k += (int64_t)gridDim.x * 64) {
-    const int64_t r = d_rec[k], i = r >> 1;
-    const Params Q = d_par[k];
-    long long n1 = 0;
-    const double p = (r & 1) ? exact_pdf(x[i], Q, K, &n1, &errf)
-                             : fallback_pdf<MODE>(x[i], Q, K, &n1, &errf);
-    ne += n1;
-    lp[i] = node_logp(p, Q, K);
-  }
-  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
-  if (COUNT) {
-    ne = wave_sum_ll(ne);
-    if (threadIdx.x == 0) atomicAdd(evals, (unsigned long long)ne);
   }
 }
 
@@ -2067,22 +2049,13 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                      node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
                      prof);
   if constexpr (MODE != kDirect) {
-    // adaptive families: the fast pass's records, one wave each, when they
-    // are sparse in their chunks (node_engine_kernel), else one wave per
-    // listed chunk (node_chunk_kernel, whose exact / walk records reuse the
-    // record buffers); each kernel reads the counts and runs only when chosen
+    // adaptive families, one launch: the fast pass's records one wave each
+    // when they are sparse in their chunks, else one wave per listed chunk
+    // (node_chunk_kernel reads the counts and picks)
     const int64_t nw = (n + 63) / 64;
-    // grids of the kernels that usually exit at once stay small: their waves
-    // carry kilobytes of scratch per lane (the exact path on one lane)
-    const int64_t nr = std::min<int64_t>(std::max<int64_t>((n + kEngBlock - 1) / kEngBlock, 1), 256);
-    hipLaunchKernelGGL((node_engine_kernel<MODE, COUNT, false>), dim3(nr), dim3(kEngBlock), 0, s,
-                       x, K, lp, d_idx, d_par, n_defer + 2, evals, status, n_defer);
     const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
-                       n, P, K, lp, clist, n_defer, d_idx, d_par, n_defer + 1, evals, prof);
-    const int64_t g = std::min<int64_t>(nw, 64);
-    hipLaunchKernelGGL((node_defer_kernel<MODE, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp, d_idx,
-                       d_par, n_defer + 1, evals, status);
+                       n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;
