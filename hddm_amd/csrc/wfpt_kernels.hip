@@ -1345,6 +1345,166 @@ __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, 
   }
 }
 
+// One-block calls of the full DDM (kAdaptTZ: 25 pdf_sv evaluations per
+// trial, the per-node drop-in call of HDDM with sv, sz, st) are one wave's
+// latency in small_kernel: 64 trials per wave, each lane its trial's 5 t
+// nodes in sequence. Here three lanes share a trial (768 threads: 3 waves per
+// SIMD, so the generic t-node code fits its registers): lane s of trial k
+// evaluates t nodes s and s + 3 (l0_node, the function the split units'
+// level-0 tasks use, bit-identical to the per-lane loop) into LDS; then waves
+// 0-3 take one trial per lane again (chunk c on wave c), run the root stop
+// test and the value from the five values as eng_level0_t does, and continue
+// exactly as small_kernel (chunk partials, zero words, deferred slots, the
+// finalize), so every output is small_kernel's, bit for bit.
+// WFPT_SMALL_SPLIT=0: small_kernel.
+#ifndef WFPT_SMALL_SPLIT
+#define WFPT_SMALL_SPLIT 1
+#endif
+#ifndef WFPT_SPLIT_LANES
+#define WFPT_SPLIT_LANES 3
+#endif
+constexpr int kSplitLanes = WFPT_SPLIT_LANES;
+constexpr int kSplitBlock = kSplitLanes * kFastBlock;
+
+// eng_level0_t's tail (KEEP_F) for one trial, from its five t-node values.
+template <int MODE>
+__device__ inline int l0_finish(const Trial& tr, const Params& P, const Knobs& K, int flags,
+                                unsigned pend, const double (&f)[5], double& p) {
+  p = 0.0;
+  if (!tr.valid) return kFinal;
+  if (flags & kFlagExact) return kExact;
+  if (pend) return kTree;
+  double lb, ub;
+  tree_root<MODE>(tr, P, lb, ub);
+  const bool structural = tr.x - lb <= 0;
+  const Simp s = simp5(ub - lb, f[0], f[1], f[2], f[3], f[4]);
+  int fl = 0;
+  const bool refine = simpson_refine(s.S, s.S2, K.simps_err, K.n_st, fl);
+  if (fl & kFlagExact) return kExact;
+  if (refine) return kTree;
+  p = s.S2 + (s.S2 - s.S) / 15;
+  if (p > kExactBelow || structural) return kFinal;
+  if (!tiny_absorbed(p, P.p_outlier, K.w_outlier)) return kExact;
+  p = 0.0;
+  return kFinal;
+}
+
+template <int MODE, int OUT>
+__global__ __launch_bounds__(kSplitBlock) void small_split_kernel(TrialArgs A, Work W,
+                                                                 RootGrids R, FinArgs F) {
+  static_assert(MODE == kAdaptTZ, "t-node split of the full DDM");
+  __shared__ double sf[5][kFastBlock];  // t-node values, node-major
+  __shared__ int sfl[kSplitLanes][kFastBlock];
+  __shared__ unsigned spd[kSplitLanes][kFastBlock];
+  __shared__ double fp[kFastBlock / 64];
+  __shared__ int fz[kFastBlock / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int k = t / kSplitLanes, sub = t - k * kSplitLanes;  // this lane's trial and share
+  const bool own = k < A.n;
+  const double x0 = own ? A.x[k] : 0.0;
+  const bool pos = x0 > 0;
+  const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
+  const int b = (bp == bo) ? 1 : 0;
+  int flags = 0;
+  unsigned pend = 0u;
+  long long ne = 0;
+  // pass 1: the lanes of boundary b (a single-boundary wave: all); pass 2: the
+  // upper-boundary lanes of a mixed wave (wave-uniform grids, as small_kernel)
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool mine = pass == 0 ? (own && pos == (b != 0)) : (bp != 0ull && bp != bo && own && pos);
+    if (!mine) continue;
+    const int bb = pass == 0 ? b : 1;
+    const Trial tr = trial_setup_b(x0, A.P, bb != 0);
+    if (!tr.valid) continue;
+    double lb, ub;
+    tree_root<MODE>(tr, A.P, lb, ub);
+    const L0Hints H = l0_hints(tr.x, lb, ub, A.P.a, A.K.err);
+#pragma unroll 1
+    for (int j = sub; j < 5; j += kSplitLanes) {
+      bool pj = false;
+      sf[j][k] = l0_node<MODE>(tr, A.P, A.K, lb, ub, H, j, zgrid_uniform(R, bb), flags, pj, ne,
+                               WFPT_SIN_TABLE ? &R.S[bb][0][0] : nullptr);
+      if (pj) pend |= 1u << (j * (kTreeW / 4));
+    }
+  }
+  if (own) {
+    sfl[sub][k] = flags;
+    spd[sub][k] = pend;
+  }
+  __syncthreads();
+  // one trial per lane again: chunk c on wave c (small_kernel's operations)
+  if (wv < kFastBlock / 64) {
+    const int i = t, c = wv;
+    if (c * 64 < A.n) {  // wave-uniform
+      const bool own1 = i < A.n;
+      int oc = kFinal;
+      double p = 0.0;
+      if (own1) {
+        const double xi = A.x[i];
+        int fl = 0;
+        unsigned pd = 0u;
+#pragma unroll
+        for (int q = 0; q < kSplitLanes; ++q) {
+          fl |= sfl[q][i];
+          pd |= spd[q][i];
+        }
+        const double f[5] = {sf[0][i], sf[1][i], sf[2][i], sf[3][i], sf[4][i]};
+        oc = l0_finish<MODE>(trial_setup_b(xi, A.P, xi > 0), A.P, A.K, fl, pd, f, p);
+      }
+      double part = 0.0;
+      int zw = 0;
+      bool tree = false;
+      if (__ballot(oc == kTree) != 0ull) {
+        if (lane == 0) W.redo[c] = 1;  // the host runs the redo pass (lean_kernel)
+        zw = kZeroDefer;
+        tree = true;
+      } else {
+        double lp = 0.0;
+        int zero = 0;
+        const bool defer = oc == kExact;
+        if (own1 && !defer) emit<OUT>(A, i, p, lp, zero);
+        const bool anyd = defer_slots(W, c, lane, defer, kFlagExact);
+        part = wave_sum(lp);
+        zw = __popcll(__ballot(zero != 0)) | (anyd ? kZeroDefer : 0);
+      }
+      if (lane == 0) {
+        if (!tree) A.out[c] = part;
+        A.zeros[c] = zw;
+        fp[wv] = part;
+        fz[wv] = zw;
+      }
+    }
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  const int nb = (int)((A.n + 63) / 64);
+  double s = 0.0;
+  long long z = 0;
+  int def = 0;
+  if (lane < nb) {
+    s += fp[lane];
+    z += fz[lane] & (kZeroDefer - 1);
+    def |= fz[lane];
+  }
+  def = F.defer_bits ? (def & kZeroDefer) : 0;
+  s = wave_sum(s);
+  z = wave_sum_ll(z);
+  const bool anyd = __ballot(def != 0) != 0ull;
+  if (lane == 0) {
+    double tt = 0.0;
+    long long zz = 0;
+    int dd = 0;
+    const double ss[2] = {s, 0.0};
+    for (int q = 0; q < 16; ++q) {
+      tt += ss[q == 0 ? 0 : 1];
+      zz += q == 0 ? z : 0ll;
+      dd |= q == 0 ? (int)anyd : 0;
+    }
+    fin_write(tt, zz, dd, F.status, F.out, F.seq, nullptr, nullptr, F.tree_any, nullptr);
+  }
+}
+
 // Copies a device result {sum, zeros, errors} (after the RCCL all-reduce) to
 // the mapped host slot, then writes the completion word.
 __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* out,
@@ -2014,8 +2174,12 @@ bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, d
                          Fa);                                                                \
       break;                                                                                 \
     default:                                                                                 \
-      hipLaunchKernelGGL((small_kernel<kAdaptTZ, O_>), dim3(1), dim3(kFastBlock), 0, s, A, F,   \
-                         R, Fa);                                                             \
+      if (WFPT_SMALL_SPLIT)                                                                  \
+        hipLaunchKernelGGL((small_split_kernel<kAdaptTZ, O_>), dim3(1), dim3(kSplitBlock), 0, s, \
+                           A, F, R, Fa);                                                     \
+      else                                                                                   \
+        hipLaunchKernelGGL((small_kernel<kAdaptTZ, O_>), dim3(1), dim3(kFastBlock), 0, s, A, F, \
+                           R, Fa);                                                           \
       break;                                                                                 \
   }
   if (trial) {

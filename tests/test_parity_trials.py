@@ -395,3 +395,30 @@ def test_small_time_table_paths(gpu, oracle_lib, case):
     for _ in range(2):  # full sequence, then the predicted one
         tot = ds.wiener_like(*args, err, 2, 2, 1, 1e-3, 0.05, 0.1)
         assert abs(tot - want) <= 1e-11 * math.fsum(np.abs(ref)), (case, tot, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("family", ["simple", "full"])
+def test_node_dataset_with_nan_rts(gpu, oracle_lib, family):
+    """NaN RTs in a node dataset: the per-node |rt| sort puts them
+    last within their node (a strict weak order), the per-trial terms come
+    back in the caller's order with NaN exactly where the reference has it
+    (its full_pdf of NaN is NaN, wfpt.pyx:66-74), and a node holding a NaN
+    sums to NaN while the others keep their sums."""
+    rng = np.random.default_rng(31 if family == "simple" else 32)
+    x, node, P = _node_dataset(rng, 9, family)
+    P[:, 7] = 0.05  # every node in range: NaN must come from the RTs alone
+    bad = rng.choice(x.size, 12, replace=False)
+    x = x.copy()
+    x[bad] = np.where(rng.random(bad.size) < 0.5, np.nan, -np.nan)
+    ds = gpu.Dataset(x, node_id=node, n_nodes=P.shape[0])
+    sums, terms = ds.wiener_like_nodes(P, *KN, trials=True)
+    ref = node_terms_ref(oracle_lib, x, node, P)
+    assert np.array_equal(np.isnan(ref), np.isnan(x))  # the reference's own semantics
+    assert_logp_parity(terms, ref, f"{family} node terms with NaN RTs")
+    for j in range(P.shape[0]):
+        tj = ref[node == j]
+        if np.isnan(tj).any():
+            assert np.isnan(sums[j]), j
+        elif tj.size:
+            assert abs(sums[j] - math.fsum(tj)) <= 1e-12 * math.fsum(np.abs(tj)) + 1e-12, j
