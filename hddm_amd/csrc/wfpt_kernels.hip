@@ -1728,116 +1728,6 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   }
 }
 
-// node_fast_kernel of the full DDM (kAdaptTZ) with the t-node split of
-// small_split_kernel: a block's 256 trials over 768 lanes, lane s of a trial
-// evaluating t nodes s and s + 3 on the trial's own root z grid (fast_level0's
-// zgrid_setup) into LDS; then one trial per lane again (the block's 4 chunks
-// on waves 0-3) for the root stop test and value (l0_finish, eng_level0_t's
-// operations), the node's term and node_fast_kernel's deferral lists. Three
-// times the waves of the per-lane pass: a config-4 call (100k trials) is
-// otherwise one wave's latency of five t nodes in sequence.
-#ifndef WFPT_NODE_SPLIT
-#define WFPT_NODE_SPLIT 1
-#endif
-template <int MODE, bool COUNT>
-__global__ __launch_bounds__(kSplitBlock) void node_fast_split_kernel(
-    const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
-    int64_t* d_idx, Params* d_par, int* n_defer, int* clist, int* n_chunks,
-    unsigned long long* evals, int* status, int* prof) {
-  static_assert(MODE == kAdaptTZ && kBlock == kFastBlock, "t-node split of the full DDM");
-  __shared__ Params rows[kStageRows];
-  __shared__ double sf[5][kBlock];
-  __shared__ int sfl[kSplitLanes][kBlock];
-  __shared__ unsigned spd[kSplitLanes][kBlock];
-  __shared__ long long sne[COUNT ? kSplitLanes : 1][kBlock];
-  const int64_t i0 = (int64_t)blockIdx.x * kBlock;
-  const int t = threadIdx.x;
-  const int first = node[i0];
-  const int last = node[(i0 + kBlock - 1 < n) ? i0 + kBlock - 1 : n - 1];
-  const int span = last - first + 1;
-  const bool staged = span <= kStageRows;
-  if (staged) {
-    const double* src = reinterpret_cast<const double*>(P + first);
-    double* dst = reinterpret_cast<double*>(rows);
-    for (int q = t; q < span * 8; q += kSplitBlock) dst[q] = src[q];
-  }
-  __syncthreads();
-  {
-    const int k = t / kSplitLanes, sub = t - k * kSplitLanes;
-    const int64_t i = i0 + k;
-    int flags = 0;
-    unsigned pend = 0u;
-    long long ne = 0;
-    if (i < n) {
-      const int nj = node[i];
-      const Params Q = staged ? rows[nj - first] : P[nj];
-      const Trial tr = trial_setup(x[i], Q);
-      if (tr.valid) {
-        const ZGrid G = zgrid_setup(tr.z - tr.sz / 2., tr.z + tr.sz / 2., tr.v, Q.sv, Q.a);
-        double lb, ub;
-        tree_root<MODE>(tr, Q, lb, ub);
-        const L0Hints H = l0_hints(tr.x, lb, ub, Q.a, K.err);
-#pragma unroll 1
-        for (int j = sub; j < 5; j += kSplitLanes) {
-          bool pj = false;
-          sf[j][k] = l0_node<MODE>(tr, Q, K, lb, ub, H, j, G, flags, pj, ne);
-          if (pj) pend |= 1u << (j * (kTreeW / 4));
-        }
-      }
-      sfl[sub][k] = flags;
-      spd[sub][k] = pend;
-      if (COUNT) sne[sub][k] = ne;
-    }
-  }
-  __syncthreads();
-  if (t >= kBlock) return;
-  const int64_t i = i0 + t;
-  const int lane = t & 63;
-  long long ne = 0;
-  bool defer = false;
-  Params Q;
-  if (i < n) {
-    const int nj = node[i];
-    Q = staged ? rows[nj - first] : P[nj];
-    int fl = 0;
-    unsigned pd = 0u;
-#pragma unroll
-    for (int q = 0; q < kSplitLanes; ++q) {
-      fl |= sfl[q][t];
-      pd |= spd[q][t];
-      if (COUNT) ne += sne[q][t];
-    }
-    const double f[5] = {sf[0][t], sf[1][t], sf[2][t], sf[3][t], sf[4][t]};
-    double p;
-    const int oc = l0_finish<MODE>(trial_setup(x[i], Q), Q, K, fl, pd, f, p);
-    if (oc == kFinal) lp[i] = node_logp(p, Q, K);
-    else defer = true;
-  }
-  const unsigned long long b = __ballot(defer);
-  if (b) {
-    // the chunk for node_chunk_kernel and the trials as records for
-    // node_engine_kernel (node_fast_kernel's lists)
-    int base = 0;
-    if (lane == 0) {
-      clist[atomicAdd(n_chunks, 1)] = (int)(i >> 6);
-      base = atomicAdd(n_chunks + 2, __popcll(b));
-    }
-    base = __shfl(base, 0, 64);
-    if (defer) {
-      const int q = base + __popcll(b & lanemask_lt(lane));
-      d_idx[q] = i;
-      d_par[q] = Q;
-    }
-  }
-  if (COUNT) {
-    ne = wave_sum_ll(defer ? 0 : ne);
-    if (lane == 0) {
-      atomicAdd(evals, (unsigned long long)ne);
-      if (b) atomicAdd(&prof[3], __popcll(b));
-    }
-  }
-}
-
 // The node path's completion of the chunks node_fast_kernel listed: one wave
 // per chunk, as the dataset engine (engine_kernel) runs a chunk, per node
 // segment of the chunk (nodes are contiguous and |rt|-ordered: a chunk holds
@@ -2319,14 +2209,9 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                                   Params* d_par, int* n_defer, int* clist,
                                   unsigned long long* evals, int* status, int* prof,
                                   hipStream_t s) {
-  if (MODE == kAdaptTZ && WFPT_NODE_SPLIT)
-    hipLaunchKernelGGL((node_fast_split_kernel<kAdaptTZ, COUNT>), dim3(blocks_for(n)),
-                       dim3(kSplitBlock), 0, s, x, node, n, P, K, lp, d_idx, d_par, n_defer, clist,
-                       n_defer, evals, status, prof);
-  else
-    hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s,
-                       x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
-                       prof);
+  hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
+                     node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
+                     prof);
   if constexpr (MODE != kDirect) {
     // adaptive families, one launch: the fast pass's records one wave each
     // when they are sparse in their chunks, else one wave per listed chunk
