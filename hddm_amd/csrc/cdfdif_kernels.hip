@@ -153,8 +153,13 @@ __device__ inline double beyond_denom(int v, double g, double a2) {
   return ((100 * g) * g) + pv;
 }
 
-// log(1 - exp(dh * (upper_t - lower_t))), dh = -denom/2 (cdfdif.c:141-142)
-__device__ inline double beyond_lx(double dh, double width) { return log(1 - exp(dh * width)); }
+// log(1 - exp(dh * (upper_t - lower_t))), dh = -denom/2 (cdfdif.c:141-142).
+// Below -40 the exponential is < 2^-54, so 1 - e rounds to 1 and the log is 0
+// exactly (in any libm): the same value without the two calls.
+__device__ inline double beyond_lx(double dh, double width) {
+  const double e = dh * width;
+  return e < -40.0 ? 0.0 : log(1 - exp(e));
+}
 
 // fact of (v, m) on boundary x (cdfdif.c:133-140)
 __device__ inline double beyond_fact(int v, int m, int x, double denom, const CdfPar& P,
@@ -435,21 +440,32 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
     const CdfTrial T = cdf_prepare(fabs(xi), xi > 0, P, S);
     double F;
     if (T.branch == 1) {
-      double h0 = 0, h1 = 0, h2 = 0;
+      // h1, h2: the last two partial sums (the reference's sequential
+      // additions, cdfdif.c:128-147). Per round the 64 additions run without
+      // a test between them (lane j keeps the sum after term j), then every
+      // lane tests its own step at once and the first converged step ends the
+      // series: the same sums and the same stopping term as one test per step.
+      double h1 = 0, h2 = 0;
       bool conv = false;
       for (int v0 = 0; v0 < kVMax && !conv; v0 += 64) {
         const int v = v0 + lane;
         const double term = v < kVMax ? beyond_term(v, T, P, S) : 0.0;
         const int m = (kVMax - v0 < 64) ? kVMax - v0 : 64;
-        for (int j = 0; j < m; ++j) {
-          h0 = h1;
-          h1 = h2;
-          h2 = h1 + __shfl(term, j, 64);
-          if (converged(h0, h1, h2)) {
-            conv = true;
-            break;
-          }
+        double h = h2, hk = 0.0;
+#pragma unroll
+        for (int j = 0; j < 64; ++j) {
+          h = h + __shfl(term, j, 64);
+          hk = lane == j ? h : hk;
         }
+        const double up1 = __shfl(hk, (lane + 63) & 63, 64), up2 = __shfl(hk, (lane + 62) & 63, 64);
+        const double hm1 = lane >= 1 ? up1 : h2;
+        const double hm2 = lane >= 2 ? up2 : (lane == 1 ? h2 : h1);
+        const unsigned long long cb = __ballot(lane < m && converged(hm2, hm1, hk));
+        const int last = cb ? __ffsll((long long)cb) - 1 : m - 1;
+        conv = cb != 0ull;
+        h1 = __shfl(hk, last > 0 ? last - 1 : 0, 64);
+        if (last == 0) h1 = h2;
+        h2 = __shfl(hk, last, 64);
       }
       F = beyond_F(h2, T, P);
     } else {
