@@ -1614,15 +1614,6 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
 // interval can be evaluated on its own (a split chunk's level-0 task) with
 // exactly the bits the per-lane loop produces. The z grid is the call's table
 // (EngTables), shared by both.
-// Per-call constants of the level-0 pass for one boundary (the lean / small
-// kernels get them from the host in RootGrids): 1/a^2, 1/(ub - lb) and the
-// Simpson weights h/6, h/12 of the t interval, 1/(z interval). The same IEEE
-// divisions of the same operands as the per-lane forms below, so the same
-// bits. A null pointer where they are passed: computed per lane.
-struct L0Const {
-  double ia2, iw, h6, h12, iZz;
-};
-
 struct L0Hints {
   // q of t node j is q0 R^j (formed per node: two registers instead of five
   // held across the node loop; the products are the ones a table would hold)
@@ -1637,8 +1628,7 @@ struct L0Hints {
     return j == 0 ? q0 : q0 * Rj;
   }
 };
-__device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, double err,
-                                   const L0Const* kc = nullptr) {
+__device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, double err) {
   L0Hints H;
   H.q0 = -1.0;
   H.R = 0.0;
@@ -1646,7 +1636,7 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
   H.D4 = Decision{0, 0, 0};
   H.ok0 = H.ok4 = H.shared = false;
   const double a2 = a * a;
-  const double ia2 = kc ? kc->ia2 : 1.0 / a2;
+  const double ia2 = 1.0 / a2;
   H.ia2 = ia2;
   // values only (the fp32 decision estimates below have a 1e-5 guard band)
   const double q0 = exp_node((-kPi2 * ((x - lb) * ia2)) * 0.5);
@@ -1670,11 +1660,10 @@ __device__ inline L0Hints l0_hints(double x, double lb, double ub, double a, dou
 template <int MODE>
 __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& K, double lb,
                                  double ub, const L0Hints& H, int j, const ZGrid& G, int& flags,
-                                 bool& pend, long long& ne, const double* stab = nullptr,
-                                 const L0Const* kc = nullptr) {
+                                 bool& pend, long long& ne, const double* stab = nullptr) {
   const double a = P.a, sv = P.sv, err = K.err;
   const double x = tr.x, v = tr.v, z = tr.z;
-  const double iw = kc ? kc->iw : 1.0 / (ub - lb);
+  const double iw = 1.0 / (ub - lb);
   const double c = (ub + lb) / 2.;
   const double d = (lb + c) / 2., e = (c + ub) / 2.;
   const double tc = j == 0 ? lb : j == 1 ? d : j == 2 ? c : j == 3 ? e : ub;
@@ -1693,7 +1682,7 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
   }
 #endif
   if (MODE == kAdaptTZ) {
-    const double iZz = kc ? kc->iZz : 1.0 / ((z + tr.sz / 2.) - (z - tr.sz / 2.));
+    const double iZz = 1.0 / ((z + tr.sz / 2.) - (z - tr.sz / 2.));
     return inner_root(T, G, iZz, v, sv, a, K, flags, ne, pend, stab) * iw;
   }
   ne += 1;
@@ -1714,8 +1703,7 @@ __device__ inline double l0_node(const Trial& tr, const Params& P, const Knobs& 
 template <int MODE, bool KEEP_F = true, bool UNROLL = false, bool LITERAL = !UNROLL>
 __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs& K,
                                    const ZGrid& G, double& p, double (&f)[5], long long& ne,
-                                   unsigned& pend, const double* stab = nullptr,
-                                   const L0Const* kc = nullptr) {
+                                   unsigned& pend, const double* stab = nullptr) {
   p = 0.0;
   pend = 0u;
   if (!tr.valid) return kFinal;
@@ -1735,21 +1723,20 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
     for (int i = 0; i < 5; ++i) f[i] = f[i] * iw;
     ne += 5;
   } else {
-    const L0Hints H = l0_hints(tr.x, lb, ub, P.a, K.err, kc);
+    const L0Hints H = l0_hints(tr.x, lb, ub, P.a, K.err);
     if (!KEEP_F) {
       // X, Y, Z after node j:  0: f0 | 1: f0, f0+4f1 | 2: f2, f0+4f2, Sl |
       // 3: f2+4f3, f0+4f2, Sl | 4: -> S = h6((f0+4f2)+f4), Sr = h12((f2+4f3)+f4)
       const double h = ub - lb;
-      const double h6 = kc ? kc->h6 : h / 6, h12 = kc ? kc->h12 : h / 12;
       double X = 0.0, Y = 0.0, Z = 0.0, y4 = 0.0;
 #define WFPT_L0_ACC_NODE(j)                                                      \
   {                                                                              \
     bool pj;                                                                     \
-    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab, kc);  \
+    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);  \
     if (flags & kFlagExact) return kExact;                                       \
     if (pj) pend |= 1u << ((j) * (kTreeW / 4));                                  \
     const double x4 = X + (4 * y);                                               \
-    if ((j) == 2) Z = h12 * (Y + y);                                             \
+    if ((j) == 2) Z = (h / 12) * (Y + y);                                        \
     Y = ((j) == 1 || (j) == 2) ? x4 : Y;                                         \
     X = ((j) == 0 || (j) == 2) ? y : ((j) == 3 ? x4 : X);                        \
     y4 = y;                                                                      \
@@ -1764,9 +1751,9 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
 #undef WFPT_L0_ACC_NODE
       if (pend) return kTree;
       Simp s;
-      s.S = h6 * (Y + y4);
+      s.S = (h / 6) * (Y + y4);
       s.Sl = Z;
-      s.Sr = h12 * (X + y4);
+      s.Sr = (h / 12) * (X + y4);
       s.S2 = s.Sl + s.Sr;
       const int bottom = K.n_st;
       const bool refine = simpson_refine(s.S, s.S2, K.simps_err, bottom, flags);
@@ -1781,7 +1768,7 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
 #define WFPT_L0_F_NODE(j)                                                        \
   {                                                                              \
     bool pj;                                                                     \
-    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab, kc);  \
+    const double y = l0_node<MODE>(tr, P, K, lb, ub, H, j, G, flags, pj, ne, stab);  \
     if (flags & kFlagExact) return kExact;                                       \
     if (pj) pend |= 1u << ((j) * (kTreeW / 4));                                  \
     if ((j) == 0) f[0] = y;                                                      \
@@ -1956,18 +1943,12 @@ __host__ __device__ inline void eng_tables(const Params& P, EngTables& T) {
 struct RootGrids {
   ZGrid G[2];
   double S[2][kSinK + 1][5];  // their large-time sine tables (sin_table)
-  L0Const c[2];               // the level-0 constants per boundary
 };
 __host__ __device__ inline void root_grids(const Params& P, RootGrids& R) {
-  // trial_setup's st / sz and tree_root's t interval (kAdaptT / kAdaptTZ)
-  const double st = (P.st < 1e-3) ? 0.0 : P.st, sz = (P.sz < 1e-3) ? 0.0 : P.sz;
-  const double lb = P.t - st / 2., ub = P.t + st / 2., h = ub - lb;
   for (int flip = 0; flip < 2; ++flip) {
     const double zf = flip ? 1. - P.z : P.z, vf = flip ? -P.v : P.v;
     R.G[flip] = zgrid_of(zf - P.sz / 2., zf + P.sz / 2., kGridRoot, vf, P.sv, P.a);
     sin_table(R.G[flip], R.S[flip]);
-    R.c[flip] = L0Const{1.0 / (P.a * P.a), 1.0 / (ub - lb), h / 6, h / 12,
-                        1.0 / ((zf + sz / 2.) - (zf - sz / 2.))};
   }
 }
 

@@ -856,14 +856,6 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 }
 #endif
 
-// the call's level-0 constants of boundary b (WFPT_L0_CONST=0: per lane)
-#ifndef WFPT_L0_CONST
-#define WFPT_L0_CONST 1
-#endif
-__device__ inline const L0Const* L0C(const RootGrids& R, int b) {
-  return WFPT_L0_CONST ? &R.c[b] : nullptr;
-}
-
 // WFPT_SIN_TABLE=0: the lean pass evaluates the large-time sines per lane
 // (the recurrence) instead of reading the call's table (same values).
 #ifndef WFPT_SIN_TABLE
@@ -900,11 +892,11 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   if (own && pos == (b != 0))
     oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, b != 0), A.P, A.K,
                                    zgrid_uniform(R, b), p, f0, ne0, pend0,
-                                   WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr, L0C(R, b));
+                                   WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
   if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
     if (own && pos)
       oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0,
-                                     ne0, pend0, WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr, L0C(R, 1));
+                                     ne0, pend0, WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
   }
   if (__ballot(oc == kTree) != 0ull) {
     if (lane == 0) {
@@ -1295,12 +1287,12 @@ __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, 
       if (own && pos == (b != 0))
         oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(
             trial_setup_b(x0, A.P, b != 0), A.P, A.K, zgrid_uniform(R, b), p, f0, ne0, pend0,
-            WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr, L0C(R, b));
+            WFPT_SIN_TABLE ? &R.S[b][0][0] : nullptr);
       if (bp != 0ull && bp != bo) {
         if (own && pos)
           oc = eng_level0_t<MODE, false, WFPT_LEAN_UNROLL != 0>(
               trial_setup_b(x0, A.P, true), A.P, A.K, R.G[1], p, f0, ne0, pend0,
-              WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr, L0C(R, 1));
+              WFPT_SIN_TABLE ? &R.S[1][0][0] : nullptr);
       }
       if (__ballot(oc == kTree) != 0ull) {
         if (lane == 0) W.redo[c] = 1;  // the host runs the redo pass (lean_kernel)
@@ -1427,12 +1419,12 @@ __global__ __launch_bounds__(kSplitBlock) void small_split_kernel(TrialArgs A, W
     if (!tr.valid) continue;
     double lb, ub;
     tree_root<MODE>(tr, A.P, lb, ub);
-    const L0Hints H = l0_hints(tr.x, lb, ub, A.P.a, A.K.err, L0C(R, bb));
+    const L0Hints H = l0_hints(tr.x, lb, ub, A.P.a, A.K.err);
 #pragma unroll 1
     for (int j = sub; j < 5; j += kSplitLanes) {
       bool pj = false;
       sf[j][k] = l0_node<MODE>(tr, A.P, A.K, lb, ub, H, j, zgrid_uniform(R, bb), flags, pj, ne,
-                               WFPT_SIN_TABLE ? &R.S[bb][0][0] : nullptr, L0C(R, bb));
+                               WFPT_SIN_TABLE ? &R.S[bb][0][0] : nullptr);
       if (pj) pend |= 1u << (j * (kTreeW / 4));
     }
   }
