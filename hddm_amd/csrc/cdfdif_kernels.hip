@@ -522,11 +522,7 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   P.nu = par[6];
   CdfTable* T = reinterpret_cast<CdfTable*>(tab);
   CdfWinTable* W = reinterpret_cast<CdfWinTable*>(tab + kCdfTableBeyond);
-  // a trial is in the window only if t - lower_t > kMinRT and t <= upper_t
-  // (cdfdif.c:118-121), i.e. st > kMinRT up to rounding: below half of it the
-  // window tables are never read
-  const int tb = P.st > 0.5 * kMinRT ? kCdfTableBlocks : 6;
-  hipLaunchKernelGGL(cdf_table_kernel, dim3(tb), dim3(64), 0, s, P, T, W);
+  hipLaunchKernelGGL(cdf_table_kernel, dim3(kCdfTableBlocks), dim3(64), 0, s, P, T, W);
   constexpr int G = WFPT_CDF_GROUP;
   const int64_t per_block = kCdfBlock / G;
   int64_t nb = (n + per_block - 1) / per_block;
