@@ -111,7 +111,79 @@ def cpu_baseline(x, budget_s):
                       f"{v1:.3e} trials/s)"}
 
 
-def pmc_summary(lib_path):
+STRESS_TRIALS = 250_000  # per set
+
+
+def stress_sets(n=STRESS_TRIALS):
+    """The refining workload MCMC proposals hit: 4 full-DDM parameter sets drawn
+    from HDDM's generator ranges (hddm/generate.py:38-46, seed 20261016; the
+    same sets as tools/stress_probe.py), RTs sampled from each model."""
+    from hddm_amd import wfpt
+    rng = np.random.default_rng(20261016)
+    np.random.seed(20261016)
+    out = []
+    for _ in range(4):
+        p = (rng.uniform(-4, 4), rng.uniform(0, 2.5), rng.uniform(0.5, 2), rng.uniform(0.4, 0.6),
+             rng.uniform(0, 0.4), rng.uniform(0.2, 0.5), rng.uniform(0, 0.35))
+        out.append((wfpt.gen_rts_from_cdf(*p, samples=n, dt=1e-3), p))
+    return out
+
+
+def stress_line(ctx, steps, warmup, lib_path):
+    """Secondary figure under the same clock (not the headline): resident
+    wiener_like calls over the 4 stress sets, trials/s = 1M trials / the summed
+    per-call times, and the in-wave engine kernel (the level-0 pass these sets
+    take) per launch from HIP events, with its executed-work fraction when
+    profiles/traffic_stress.json was measured on this build."""
+    from hddm_amd import wfpt
+    kn = knobs_tuple()
+    call_s, k_ms, nl, evals, ntr = 0.0, 0.0, 0, 0, 0
+    for x, p in stress_sets():
+        ds = wfpt.Dataset(x)
+        ctx.profile(ctx.PROF_EVALS)
+        ds.wiener_like(*p, *kn)
+        _, _, ne = ctx.profile_read(reset=True)
+        ctx.profile(0)
+        evals += ne
+        ntr += x.size
+        for _ in range(warmup):
+            ds.wiener_like(*p, *kn)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ds.wiener_like(*p, *kn)
+        ctx.synchronize()
+        call_s += (time.perf_counter() - t0) / steps
+        ctx.profile(ctx.PROF_EVENTS)
+        ctx.profile_read(reset=True)
+        for _ in range(steps):
+            ds.wiener_like(*p, *kn)
+        ctx.synchronize()
+        km, l, _ = ctx.profile_read(reset=True)
+        ctx.profile(0)
+        k_ms += km / max(l, 1)
+        nl += 1
+        ds.close()
+    k_avg_s = k_ms / nl / 1e3
+    out = {"workload": "4 x 250k full-DDM trials, parameters from hddm/generate.py:38-46 "
+                       "ranges (seed 20261016), one resident wiener_like call per set",
+           "trials_per_s": ntr / call_s, "ms_per_1M_trials": call_s * 1e3 * 1e6 / ntr,
+           "pdf_sv_evals_per_trial": evals / ntr,
+           "kernel": "wfpt::engine_kernel<3, false, 0> (in-wave adaptive engine)",
+           "kernel_ms_avg": k_avg_s * 1e3, "frac": None}
+    pmc = pmc_summary(lib_path, "traffic_stress.json")
+    if pmc and pmc.get("matches_build"):
+        w = float(pmc["fp64_lane_ops_per_trial"])
+        ach = STRESS_TRIALS * w / k_avg_s / 1e12
+        tr = pmc.get("hbm_bytes_per_trial")
+        out.update(achieved=ach, frac=ach / (PEAK_LANE_OPS / 1e12), fp64_lane_ops_per_trial=w,
+                   valu_issue_utilisation=pmc.get("valu_issue_utilisation"),
+                   traffic=tr * STRESS_TRIALS if tr is not None else None,
+                   algorithmic_bytes=8.0 * STRESS_TRIALS, pmc_source=pmc.get("source"))
+    return out
+
+
+def pmc_summary(lib_path, name="traffic.json"):
     """Executed-work figures of the dominant kernel from the committed rocprofv3
     PMC summary (profiles/traffic.json, written by tools/summarize_profile.py),
     used only if it was measured on a library built from the same sources and
@@ -119,7 +191,7 @@ def pmc_summary(lib_path):
     time next to the .so). Per-trial figures: the C3 and C5 datasets are
     samples of the same model."""
     from hddm_amd import build as hb
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+    path = os.path.join(ROOT, "profiles", name)
     if not os.path.exists(path):
         return None
     try:
@@ -155,6 +227,8 @@ def main():
                     help="trials per GPU (default: C3 1M at N=1, C5 100M/N at N>1)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stress", action="store_true",
+                    help="skip the secondary stress-set figure (N = 1 only)")
     a = ap.parse_args()
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -278,6 +352,8 @@ def main():
                    "logp": val},
         "roofline": roof,
     }
+    if world == 1 and not a.no_stress:
+        out["stress"] = stress_line(ctx, a.steps, a.warmup, _lib.LIB_PATH)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(x, a.cpu_seconds)
     if rank == 0:

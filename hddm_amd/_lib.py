@@ -116,10 +116,11 @@ wfpt_last_path = _sig("wfpt_last_path", _I, [_VP, ctypes.POINTER(_I)])
 wfpt_wiener_like_local = _sig("wfpt_wiener_like_local", _I, [_VP, _VP, _PP, _PK, _PD])
 wfpt_wiener_like_nodes_local = _sig("wfpt_wiener_like_nodes_local", _I, [_VP, _VP, _PP, _PK, _PD])
 wfpt_wiener_like_nodes_allreduce = _sig("wfpt_wiener_like_nodes_allreduce", _I,
-                                        [_VP, _VP, _PP, _PK, _PD])
+                                        [_VP, _VP, _PP, _I32, _PK, _PD])
 # WFPT_PATH_* (include/wfpt_amd.h): kernels the last likelihood call launched
 PATH_LEAN, PATH_ENGINE, PATH_SMALL, PATH_REDO = 1, 2, 4, 8
 PATH_FOLD, PATH_DIRECT, PATH_FIXED, PATH_SPLIT = 16, 32, 64, 128
+PATH_SMALL_SPLIT = 256
 wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
 EXPORTED = [

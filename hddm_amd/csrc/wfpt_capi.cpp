@@ -216,9 +216,10 @@ struct wfpt_ds {
   int* hzn = nullptr;
   mutable int nsplit = 0;  // chunks the next call splits
   mutable int parity = 0;
-  // the caller's index of each stored trial (per-trial outputs are returned
-  // in the caller's order); empty = identity (WFPT_DS_INPUT_ORDER)
-  std::vector<int64_t> perm;
+  // device: the caller's index of each stored trial (per-trial outputs of the
+  // diagnostic calls are returned in the caller's order; kept in HBM, not in
+  // host memory: 8 B per trial); null = identity (WFPT_DS_INPUT_ORDER)
+  int64_t* perm = nullptr;
 };
 
 namespace {
@@ -401,12 +402,16 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
                                             ? part == (wfpt::kPassFast | wfpt::kPassLean)
                                             : part == wfpt::kPassFast);
   const bool direct = adaptive && !engine_family(P, K);
-  if (c->small && level0_only && !prof && !c->count && !mirror &&
-      wfpt::launch_small(dx, n, P, K, c->part.p, c->zero.p, c->status, W, out, ++c->seq,
-                         c->tree_any, c->stream, c->trial)) {
-    HIP_TRY(hipGetLastError());
-    c->path |= WFPT_PATH_SMALL | (direct ? WFPT_PATH_DIRECT : WFPT_PATH_LEAN);
-    return WFPT_OK;
+  if (c->small && level0_only && !prof && !c->count && !mirror) {
+    const int sk = wfpt::launch_small(dx, n, P, K, c->part.p, c->zero.p, c->status, W, out,
+                                      c->seq + 1, c->tree_any, c->stream, c->trial);
+    if (sk != wfpt::kSmallNone) {
+      ++c->seq;
+      HIP_TRY(hipGetLastError());
+      c->path |= WFPT_PATH_SMALL | (direct ? WFPT_PATH_DIRECT : WFPT_PATH_LEAN) |
+                 (sk == wfpt::kSmallSplit ? WFPT_PATH_SMALL_SPLIT : 0);
+      return WFPT_OK;
+    }
   }
   const wfpt::Split S = eng ? split_of(d) : wfpt::Split{};
   wfpt::launch_trials(c->trial ? 3 : 0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p,
@@ -568,6 +573,22 @@ bool abs_less_nan_last(double a, double b) {
   const bool na = std::isnan(a), nb = std::isnan(b);
   if (na || nb) return !na && nb;
   return std::fabs(a) < std::fabs(b);
+}
+
+// Per-trial values of a dataset's stored order (device) -> the caller's order
+// (host) through the dataset's stored permutation (diagnostic calls only).
+int trials_to_caller(const wfpt_ds* d, const double* dev, double* out) {
+  if (d->n <= 0) return WFPT_OK;
+  std::vector<double> h(d->n);
+  HIP_TRY(hipMemcpy(h.data(), dev, d->n * sizeof(double), hipMemcpyDeviceToHost));
+  if (!d->perm) {
+    std::memcpy(out, h.data(), d->n * sizeof(double));
+    return WFPT_OK;
+  }
+  std::vector<int64_t> perm(d->n);
+  HIP_TRY(hipMemcpy(perm.data(), d->perm, d->n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < d->n; ++i) out[perm[i]] = h[i];
+  return WFPT_OK;
 }
 
 int upload(wfpt_ctx* c, const double* x, int64_t n) {
@@ -766,12 +787,15 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
   auto* d = new wfpt_ds();
   d->ctx = c;
   d->n = n;
-  if (!keep_order || node_id) d->perm = idx;
   d->input_order = (flags & WFPT_DS_INPUT_ORDER) != 0;
   d->n_nodes = node_id ? n_nodes : 0;
   hipError_t e = hipMalloc((void**)&d->x, std::max<int64_t>(n, 1) * sizeof(double));
   if (e == hipSuccess && n > 0)
     e = hipMemcpy(d->x, hx.data(), n * sizeof(double), hipMemcpyHostToDevice);
+  if (e == hipSuccess && (!keep_order || node_id) && n > 0) {
+    e = hipMalloc((void**)&d->perm, n * sizeof(int64_t));
+    if (e == hipSuccess) e = hipMemcpy(d->perm, idx.data(), n * sizeof(int64_t), hipMemcpyHostToDevice);
+  }
   if (e == hipSuccess && node_id) {
     e = hipMalloc((void**)&d->node, std::max<int64_t>(n, 1) * sizeof(int32_t));
     if (e == hipSuccess && n > 0)
@@ -812,6 +836,8 @@ void ds_free_device(wfpt_ds* d) {
   if (d->x) (void)hipFree(d->x);
   if (d->node) (void)hipFree(d->node);
   if (d->off) (void)hipFree(d->off);
+  if (d->perm) (void)hipFree(d->perm);
+  d->perm = nullptr;
   for (int k = 0; k < 2; ++k) {
     if (d->hpred[k]) (void)hipFree(d->hpred[k]);
     if (d->hlist[k]) (void)hipFree(d->hlist[k]);
@@ -891,19 +917,18 @@ int wfpt_wiener_like_trials(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
   }
   c->trial = nullptr;
   if (rc != WFPT_OK) return rc;
-  if (d->n > 0) {
-    std::vector<double> h(d->n);
-    HIP_TRY(hipMemcpy(h.data(), c->lp.p, d->n * sizeof(double), hipMemcpyDeviceToHost));
-    if (d->perm.empty()) std::memcpy(out_trial, h.data(), d->n * sizeof(double));
-    else
-      for (int64_t i = 0; i < d->n; ++i) out_trial[d->perm[i]] = h[i];
-  }
-  return WFPT_OK;
+  return trials_to_caller(d, c->lp.p, out_trial);
 }
 
 int wfpt_dataset_order(const wfpt_ds* d, int64_t* perm) {
   if (!d || (!perm && d->n > 0)) return fail(WFPT_ERR_ARG, "null pointer");
-  for (int64_t i = 0; i < d->n; ++i) perm[i] = d->perm.empty() ? i : d->perm[i];
+  if (!d->ctx) return fail(WFPT_ERR_ARG, "the dataset's context was closed");
+  if (!d->perm) {
+    for (int64_t i = 0; i < d->n; ++i) perm[i] = i;
+    return WFPT_OK;
+  }
+  DeviceGuard g(d->ctx->device);
+  HIP_TRY(hipMemcpy(perm, d->perm, d->n * sizeof(int64_t), hipMemcpyDeviceToHost));
   return WFPT_OK;
 }
 
@@ -1056,13 +1081,9 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   }
   if (int rc = finish_profile(c)) return rc;
   std::memcpy(out, c->mnode.h, m * sizeof(double));
-  if (out_trial && d->n > 0) {
-    // each trial's term (node_logp: the node's mixture, log, -inf for a zero
-    // density or p_outlier outside [0, 1]) in the caller's trial order
-    std::vector<double> h(d->n);
-    HIP_TRY(hipMemcpy(h.data(), c->lp.p, d->n * sizeof(double), hipMemcpyDeviceToHost));
-    for (int64_t i = 0; i < d->n; ++i) out_trial[d->perm[i]] = h[i];
-  }
+  // each trial's term (node_logp: the node's mixture, log, -inf for a zero
+  // density or p_outlier outside [0, 1]) in the caller's trial order
+  if (out_trial) return trials_to_caller(d, c->lp.p, out_trial);
   return WFPT_OK;
 }
 
@@ -1084,17 +1105,31 @@ int wfpt_wiener_like_nodes_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_param
 }
 
 int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
-                                     const wfpt_knobs* k, double* out) {
+                                     int32_t n_nodes, const wfpt_knobs* k, double* out) {
   if (!c) return fail(WFPT_ERR_ARG, "null context");
   if (!c->comm) return fail(WFPT_ERR_ARG, "wfpt_comm_init was not called");
+  // the exchange's count comes from the argument every rank passes, never
+  // from this rank's dataset: a rank with a bad dataset still all-reduces
+  // the same n_nodes + 1 doubles as its peers
+  if (n_nodes < 0) return fail(WFPT_ERR_ARG, "n_nodes < 0 (no exchange entered)");
   WFPT_RANGE("wfpt_wiener_like_nodes_allreduce");
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   // every exit once the communicator exists goes through the exchange: a
   // rank whose pass fails enters it with a poisoned vector
   int lrc = nodes_check(c, d, per_node, k, out);
-  const int32_t m = d && d->ctx == c ? d->n_nodes : 0;
+  const int32_t m = n_nodes;
+  if (lrc == WFPT_OK && d->n_nodes != n_nodes)
+    lrc = fail(WFPT_ERR_ARG, "dataset has " + std::to_string(d->n_nodes) +
+                                 " nodes, the call passes n_nodes = " + std::to_string(n_nodes));
   if (lrc == WFPT_OK) lrc = nodes_launch(c, d, per_node, to_knobs(k));
+  // fault injection for the failure path's tests (WFPT_FAULT=nodes_allreduce_local:
+  // this rank's per-node pass reports a failure after it was enqueued)
+  if (lrc == WFPT_OK) {
+    const char* fi = std::getenv("WFPT_FAULT");
+    if (fi && std::strcmp(fi, "nodes_allreduce_local") == 0)
+      lrc = fail(WFPT_ERR_HIP, "injected local failure (WFPT_FAULT=nodes_allreduce_local)");
+  }
   std::string lmsg = lrc != WFPT_OK ? g_last_error : std::string();
   if (c->res.cap < (size_t)m + 1) {  // the node vector of an early failure
     if (c->res.reserve((size_t)m + 1) != hipSuccess) {
@@ -1104,8 +1139,8 @@ int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_p
                                 "(RCCL communicator aborted)");
     }
   }
-  wfpt::launch_segment_res(lrc == WFPT_OK ? c->lp.p : nullptr, d ? d->off : nullptr, m, c->res.p,
-                           c->status, lrc != WFPT_OK, c->stream);
+  wfpt::launch_segment_res(lrc == WFPT_OK ? c->lp.p : nullptr, lrc == WFPT_OK ? d->off : nullptr,
+                           m, c->res.p, c->status, lrc != WFPT_OK, c->stream);
   if (hipGetLastError() != hipSuccess) {
     (void)ncclCommAbort(c->comm);
     c->comm = nullptr;
@@ -1565,6 +1600,18 @@ int wfpt_wiener_like_allreduce_group(wfpt_ctx* const* ctxs, const wfpt_ds* const
     double vi = 0.0;
     rc = ar_finish(ctxs[i], dss[i], st[i], &vi);
     if (i == 0) v = vi;
+  }
+  if (rc != WFPT_OK) {
+    // as the single-context path: a device whose passes were enqueued may
+    // hold a half-written heavy-chunk record; every such dataset restarts
+    // from the full call sequence
+    const std::string msg = g_last_error;
+    for (int i = 0; i < n; ++i) {
+      if (!st[i].launched) continue;
+      (void)hipSetDevice(ctxs[i]->device);
+      ar_reset(ctxs[i], dss[i]);
+    }
+    g_last_error = msg;
   }
   (void)hipSetDevice(prev);
   if (rc == WFPT_OK) *out = v;

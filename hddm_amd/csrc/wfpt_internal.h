@@ -101,11 +101,14 @@ void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer
                      double* fin = nullptr, int* ticket = nullptr);
 // One-block call (n <= 256, direct or adaptive family, level-0 pass + the
 // finalize in one launch: the same result bits and completion word as
-// launch_trials(kPassFast [| kPassLean]) + launch_finalize). false: not
-// eligible, nothing launched. trial (nullable): out_kind 3's per-trial terms.
-bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                  int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
-                  int* tree_any, hipStream_t s, double* trial = nullptr);
+// launch_trials(kPassFast [| kPassLean]) + launch_finalize). kSmallNone: not
+// eligible, nothing launched; kSmallOne: small_kernel; kSmallSplit: the full
+// DDM's small_split_kernel (three lanes per trial). trial (nullable): out_kind
+// 3's per-trial terms.
+constexpr int kSmallNone = 0, kSmallOne = 1, kSmallSplit = 2;
+int launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                 int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
+                 int* tree_any, hipStream_t s, double* trial = nullptr);
 // fin (device, 3 * 64 doubles) + ticket (device int, 0 at rest): scratch of the
 // multi-block finalize for large nb (nullptr: one block)
 // res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then
@@ -115,11 +118,12 @@ void launch_publish(const double* res, double* out, unsigned long long seq, hipS
 // (one thread, stream order: the all-reduce of a rank whose local pass failed)
 void launch_poison(double* res, hipStream_t s);
 // mode: the integration family shared by every node (kDirect..kAdaptTZ: the
-// two-pass fast path; n_defer[0..1] must be 0 on the stream: the direct
+// two-pass fast path; n_defer[0..2] must be 0 on the stream: the direct
 // family's deferred (index, row) records in d_idx / d_par (up to n) counted in
 // n_defer[0]; the adaptive families' listed chunks in clist (up to
-// (n + 63) / 64) counted in n_defer[0] and the records their chunk engine
-// hands on in d_idx / d_par counted in n_defer[1]), or -1 (mixed /
+// (n + 63) / 64) counted in n_defer[0] and the fast pass's deferred trials as
+// (index, row) records in d_idx / d_par counted in n_defer[2]; n_defer[1] is
+// unused), or -1 (mixed /
 // fixed Simpson: one generic per-trial kernel with a per-lane mode). prof
 // (COUNT builds, evals != null): the node tallies of wfpt_profile_lists.
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,

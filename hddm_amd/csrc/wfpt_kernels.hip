@@ -2147,12 +2147,12 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
   }
 }
 
-bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
-                  int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
-                  int* tree_any, hipStream_t s, double* trial) {
-  if (n <= 0 || n > kFastBlock) return false;
+int launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
+                 int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
+                 int* tree_any, hipStream_t s, double* trial) {
+  if (n <= 0 || n > kFastBlock) return kSmallNone;
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
-  if (mode > kAdaptTZ) return false;
+  if (mode > kAdaptTZ) return kSmallNone;
   const TrialArgs A = trial_args(x, n, P, K, part, zeros, nullptr, status, 0, trial);
   Work F = W;
   F.redo = mode == kDirect ? nullptr : W.redo;
@@ -2188,7 +2188,7 @@ bool launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, d
     SMALL_MODES(OUT_SUM)
   }
 #undef SMALL_MODES
-  return true;
+  return (mode == kAdaptTZ && WFPT_SMALL_SPLIT) ? kSmallSplit : kSmallOne;
 }
 
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,

@@ -1,16 +1,19 @@
 // wfpt_rendezvous.cpp — torch-free exchange of the RCCL unique id (128 bytes)
 // between the ranks of one job over TCP (POSIX sockets only).
 //
-// Rank 0 listens on the wildcard address of host's family at `port` (so peers
-// reach it whatever address the name resolves to locally, e.g. 127.0.1.1 from
-// /etc/hosts) and sends its 128-byte id to each of the nranks - 1 peers that
-// connect; every other rank connects (non-blocking, retrying until the
-// deadline: rank 0 may start later) and reads the id. A peer identifies
-// itself with a 16-byte hello {magic, nranks, rank} that rank 0 checks, so a
-// stray connection or a job with another world size is rejected instead of
-// silently joining, and acknowledges the id with one byte: rank 0 counts a
-// peer as served only after its ack (a peer whose read failed reconnects).
-// Nothing here touches the GPU.
+// Rank 0 listens on the address `host` resolves to at `port` (WFPT_COMM_BIND=any:
+// the wildcard address of its family instead, for hosts whose name resolves
+// to a loopback alias locally, e.g. 127.0.1.1 from /etc/hosts) and sends its
+// 128-byte id to each of the nranks - 1 peers that connect; every other rank
+// connects (non-blocking, retrying until the deadline: rank 0 may start
+// later) and reads the id. A peer identifies itself with a 16-byte hello
+// {magic, nranks, rank, token} that rank 0 checks (token: a hash of
+// $WFPT_COMM_TOKEN, 0 when unset), so a stray connection or a job with another
+// world size or token is rejected instead of silently joining, and
+// acknowledges the id with one byte: rank 0 counts a peer as served only after
+// its ack (a peer whose read failed reconnects). Each accepted connection gets
+// at most kPeerMs for its hello and ack, so a silent client cannot hold the
+// rendezvous until the global deadline. Nothing here touches the GPU.
 #include <arpa/inet.h>
 #include <errno.h>
 #include <fcntl.h>
@@ -22,8 +25,10 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -37,6 +42,7 @@ namespace {
 
 constexpr uint32_t kMagic = 0x77667074u;  // "wfpt"
 constexpr unsigned char kAck = 0x5a;
+constexpr int kPeerMs = 2000;  // per-connection budget of rank 0's hello / ack reads
 using Clock = std::chrono::steady_clock;
 
 struct Fd {
@@ -84,7 +90,22 @@ bool resolve(const char* host, int port, sockaddr_storage* sa, socklen_t* len) {
   return true;
 }
 
-// The wildcard address of family `fam` at `port` (rank 0's listening socket).
+// FNV-1a of $WFPT_COMM_TOKEN (0 when unset): the job token of the hello.
+uint32_t job_token() {
+  const char* t = std::getenv("WFPT_COMM_TOKEN");
+  if (!t || !*t) return 0u;
+  uint32_t h = 2166136261u;
+  for (; *t; ++t) h = (h ^ (unsigned char)*t) * 16777619u;
+  return h ? h : 1u;
+}
+
+bool bind_any() {
+  const char* b = std::getenv("WFPT_COMM_BIND");
+  return b && std::strcmp(b, "any") == 0;
+}
+
+// The wildcard address of family `fam` at `port` (rank 0's listening socket
+// under WFPT_COMM_BIND=any).
 socklen_t wildcard(int fam, int port, sockaddr_storage* sa) {
   std::memset(sa, 0, sizeof(*sa));
   if (fam == AF_INET6) {
@@ -136,8 +157,9 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
   if (!resolve(host, port, &sa, &slen))
     return wfpt_rdv_fail(WFPT_ERR_COMM, std::string("rendezvous: cannot resolve ") + host);
   if (rank == 0) {
-    sockaddr_storage la{};
-    const socklen_t llen = wildcard(sa.ss_family, port, &la);
+    sockaddr_storage la = sa;
+    socklen_t llen = slen;
+    if (bind_any()) llen = wildcard(sa.ss_family, port, &la);
     Fd ls;
     ls.fd = ::socket(la.ss_family, SOCK_STREAM, 0);
     if (ls.fd < 0) return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: socket() failed");
@@ -159,17 +181,18 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
       Fd c;
       c.fd = ::accept(ls.fd, nullptr, nullptr);
       if (c.fd < 0) continue;
+      const auto peer_deadline = std::min(deadline, Clock::now() + std::chrono::milliseconds(kPeerMs));
       uint32_t hello[4] = {0, 0, 0, 0};
-      if (!io_all(c.fd, hello, sizeof(hello), false, deadline)) continue;
+      if (!io_all(c.fd, hello, sizeof(hello), false, peer_deadline)) continue;
       const int pr_rank = (int)hello[2];
       if (hello[0] != kMagic || (int)hello[1] != nranks || pr_rank <= 0 || pr_rank >= nranks ||
-          seen[pr_rank])
+          seen[pr_rank] || hello[3] != job_token())
         continue;  // not one of this job's peers: ignored
       unsigned char ack = 0;
       // served only once the peer confirms it holds the id (otherwise it
       // reconnects and is served again)
-      if (!io_all(c.fd, id, 128, true, deadline) || !io_all(c.fd, &ack, 1, false, deadline) ||
-          ack != kAck)
+      if (!io_all(c.fd, id, 128, true, peer_deadline) ||
+          !io_all(c.fd, &ack, 1, false, peer_deadline) || ack != kAck)
         continue;
       seen[pr_rank] = true;
       ++got;
@@ -181,7 +204,7 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
     c.fd = ::socket(sa.ss_family, SOCK_STREAM, 0);
     if (c.fd < 0) return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: socket() failed");
     if (connect_by(c.fd, sa, slen, deadline)) {
-      const uint32_t hello[4] = {kMagic, (uint32_t)nranks, (uint32_t)rank, 0};
+      const uint32_t hello[4] = {kMagic, (uint32_t)nranks, (uint32_t)rank, job_token()};
       unsigned char buf[128];
       unsigned char ack = kAck;
       if (io_all(c.fd, (void*)hello, sizeof(hello), true, deadline) &&

@@ -311,7 +311,8 @@ class Dataset:
         K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = np.empty(self.n_nodes, dtype=np.float64)
         _lib.check(_lib.wfpt_wiener_like_nodes_allreduce(self.ctx.handle, self.handle, table,
-                                                         ctypes.byref(K), _lib.dptr(out)))
+                                                         self.n_nodes, ctypes.byref(K),
+                                                         _lib.dptr(out)))
         return out
 
     def wiener_like_nodes(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,

@@ -213,10 +213,15 @@ int wfpt_wiener_like_local(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *
  * partial sums plus the encoded error count (n_nodes + 1 doubles) are summed
  * with one ncclAllReduce, and every rank receives the per-node totals of all
  * trials in out_logp[n_nodes] (a node with a zero-density trial on any rank is
- * -inf). Failure semantics as wfpt_wiener_like_allreduce. */
+ * -inf). n_nodes is the length of per_node, the same on every rank; the
+ * exchange's count is taken from it, never from the dataset, so a rank whose
+ * dataset is bad (null, another context's, without node ids, or with another
+ * node count: WFPT_ERR_ARG) still enters the same n_nodes + 1 exchange,
+ * poisoned. Failure semantics otherwise as wfpt_wiener_like_allreduce;
+ * n_nodes < 0 returns WFPT_ERR_ARG before any collective. */
 int wfpt_wiener_like_nodes_allreduce(wfpt_ctx *ctx, const wfpt_ds *ds,
-                                     const wfpt_params *per_node, const wfpt_knobs *k,
-                                     double *out_logp);
+                                     const wfpt_params *per_node, int32_t n_nodes,
+                                     const wfpt_knobs *k, double *out_logp);
 /* This rank's part of that exchange, for a caller with its own collective:
  * out[n_nodes + 1] = the per-node partial sums of its shard and the encoded
  * error count (sum over ranks, then a nonzero last entry decodes as in
@@ -280,6 +285,8 @@ int wfpt_debug_partials(wfpt_ctx *ctx, double *part, int32_t *zero, int64_t n);
 #define WFPT_PATH_DIRECT 32  /* simple-DDM level 0 (fast_kernel) */
 #define WFPT_PATH_FIXED 64   /* fixed Simpson (trial_kernel) */
 #define WFPT_PATH_SPLIT 128  /* heavy chunks split into one-wave units */
+#define WFPT_PATH_SMALL_SPLIT 256 /* the full DDM's one-block call, three lanes per
+                                     trial (small_split_kernel; with WFPT_PATH_SMALL) */
 int wfpt_last_path(wfpt_ctx *ctx, int *path);
 int wfpt_synchronize(wfpt_ctx *ctx);
 

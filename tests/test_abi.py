@@ -128,5 +128,5 @@ def test_new_entry_points_reject_null_arguments_without_gpu():
     assert _lib.wfpt_last_path(None, None) == two
     assert _lib.wfpt_wiener_like_local(None, None, None, None, None) == two
     assert _lib.wfpt_wiener_like_nodes_local(None, None, None, None, None) == two
-    assert _lib.wfpt_wiener_like_nodes_allreduce(None, None, None, None, None) == two
+    assert _lib.wfpt_wiener_like_nodes_allreduce(None, None, None, 0, None, None) == two
     assert b"null" in _lib.wfpt_last_error()

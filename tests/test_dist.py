@@ -248,6 +248,50 @@ def test_tcp_rendezvous_hands_rank0_id_to_every_rank(world):
         assert r["torch"] is False
 
 
+def test_tcp_rendezvous_survives_silent_and_foreign_clients():
+    """rank 0 serves its peer although a client that connects and
+    never speaks, and one that sends a valid-looking hello with another job
+    token, reach it first: the silent one is dropped after its per-connection
+    budget (well before the deadline), the foreign one is ignored, and the
+    real peer (same WFPT_COMM_TOKEN) gets rank 0's id."""
+    import json
+    import socket
+    import struct
+    import subprocess
+    import sys
+    import time
+    port = _free_port()
+    uid = bytes(range(128))
+    env = dict(os.environ, WFPT_COMM_TOKEN="job-a")
+    p0 = subprocess.Popen([sys.executable, "-c", _RDV_CHILD, ROOT, "0", "2", str(port), uid.hex()],
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    t0 = time.time()
+    silent = None
+    while silent is None and time.time() - t0 < 60:
+        try:
+            silent = socket.create_connection(("127.0.0.1", port), timeout=1)
+        except OSError:
+            time.sleep(0.05)
+    assert silent is not None
+    foreign = socket.create_connection(("127.0.0.1", port), timeout=5)
+    foreign.sendall(struct.pack("<4I", 0x77667074, 2, 1, 12345))
+    p1 = subprocess.Popen([sys.executable, "-c", _RDV_CHILD, ROOT, "1", "2", str(port), uid.hex()],
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+    outs = [p.communicate(timeout=120) for p in (p0, p1)]
+    for p, (o, e) in zip((p0, p1), outs):
+        assert p.returncode == 0, e
+        assert bytes.fromhex(json.loads(o.strip().splitlines()[-1])["id"]) == uid
+    assert time.time() - t0 < 40  # not held until the 60 s deadline
+    foreign.settimeout(1)
+    try:
+        got = foreign.recv(128)
+    except OSError:
+        got = b""
+    assert got == b""  # the foreign hello never received the id
+    silent.close()
+    foreign.close()
+
+
 def test_tcp_rendezvous_times_out_without_rank0():
     """A peer whose rank 0 never shows up fails with an error naming the
     rendezvous (no hang past its deadline)."""
@@ -429,3 +473,43 @@ def test_rccl_single_rank_node_allreduce(gpu):
     a = ds.wiener_like_nodes(params)
     b = ds.wiener_like_nodes_allreduce(params)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_rccl_node_allreduce_failure_paths(gpu, monkeypatch):
+    """the node all-reduce's failure paths on world-1 RCCL. A
+    local failure injected after the per-node pass was enqueued
+    (WFPT_FAULT=nodes_allreduce_local) and a dataset whose node count differs
+    from the call's n_nodes both enter the exchange poisoned (node_poison_kernel,
+    node_status_kernel with poison) with the call's count, decode the
+    failure and return the rank's own error; the communicator stays usable
+    and the next call equals wiener_like_nodes bit for bit."""
+    import ctypes
+    from hddm_amd import _lib, dist as hdist
+    ctx = _lib.context()
+    hdist.init_comm(ctx, 0, 1)
+    rng = np.random.default_rng(16)
+    m = 24
+    node = rng.integers(0, m, 5000).astype(np.int32)
+    x = rng.choice([-1.0, 1.0], node.size) * (0.34 + rng.gamma(2.0, 0.4, node.size))
+    params = np.tile([0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1, 0.05], (m, 1))
+    params[:, 0] += 0.01 * np.arange(m)
+    ds = gpu.Dataset(x, node_id=node, n_nodes=m)
+    want = ds.wiener_like_nodes(params)
+    monkeypatch.setenv("WFPT_FAULT", "nodes_allreduce_local")
+    with pytest.raises(RuntimeError, match="injected local failure"):
+        ds.wiener_like_nodes_allreduce(params)
+    monkeypatch.delenv("WFPT_FAULT")
+    assert np.array_equal(ds.wiener_like_nodes_allreduce(params), want)
+    # a count that disagrees with the dataset: WFPT_ERR_ARG after the exchange
+    big = np.vstack([params, params[:1]])
+    table = (_lib.Params * (m + 1)).from_buffer_copy(np.ascontiguousarray(big).tobytes())
+    K = _lib.make_knobs(1e-4, 2, 2, 1, 1e-3, 0.1)
+    out = np.empty(m + 1)
+    rc = _lib.wfpt_wiener_like_nodes_allreduce(ctx.handle, ds.handle, table, m + 1,
+                                               ctypes.byref(K), _lib.dptr(out))
+    assert rc == 2 and b"nodes" in _lib.wfpt_last_error()
+    rc = _lib.wfpt_wiener_like_nodes_allreduce(ctx.handle, None, table, m + 1, ctypes.byref(K),
+                                               _lib.dptr(out))
+    assert rc == 2
+    assert np.array_equal(ds.wiener_like_nodes_allreduce(params), want)

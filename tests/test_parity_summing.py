@@ -85,7 +85,8 @@ def path_names(bits):
     from hddm_amd import _lib
     names = {_lib.PATH_LEAN: "lean", _lib.PATH_ENGINE: "engine", _lib.PATH_SMALL: "small",
              _lib.PATH_REDO: "redo", _lib.PATH_FOLD: "fold", _lib.PATH_DIRECT: "direct",
-             _lib.PATH_FIXED: "fixed", _lib.PATH_SPLIT: "split"}
+             _lib.PATH_FIXED: "fixed", _lib.PATH_SPLIT: "split",
+             _lib.PATH_SMALL_SPLIT: "small_split"}
     return {v for k, v in names.items() if bits & k}
 
 
@@ -124,6 +125,57 @@ def test_lean_kernel_per_trial_on_bench_dataset(gpu, oracle_lib):
     dmax = assert_terms(terms, ref, "bench C3 1M")
     assert_chunks(ctx, ds, ref, "bench C3 1M")
     assert dmax < 1e-9  # observed ~1e-14: far inside the bar
+
+
+@pytest.mark.gpu
+def test_c2_direct_kernel_per_trial_10m(gpu, oracle_lib):
+    """C2's timed kernel at dataset scale: the 10M simple-DDM resident dataset
+    (tests/test_parity_strict.py's C2 data) through fast_kernel<kDirect>'s
+    OUT_BOTH build. Its chunk partials and total are bitwise the plain call's,
+    each term is within 1e-6 of the reference's addend (src/wfpt.pyx:66-74),
+    and every one of the plain call's 156,250 chunk partials is within 1e-12
+    of fsum of the reference's 64 terms."""
+    np.random.seed(20261015)
+    x = gpu.gen_rts_from_cdf(*SIMPLE, samples=10_000_000, dt=1e-3)
+    ref = ref_terms(oracle_lib, x, SIMPLE)
+    from hddm_amd import _lib
+    ctx = _lib.context()
+    ds = gpu.Dataset(x)
+    ds.wiener_like(*SIMPLE, *KN)
+    tot, terms, path = summing_vs_trials(ctx, ds, SIMPLE)
+    assert path_names(path) == {"direct"}, path_names(path)
+    dmax = assert_terms(terms, ref, "C2 10M")
+    assert dmax < 1e-9
+    assert_chunks_fast(ctx, ds, ref, "C2 10M")
+    ds.close()
+
+
+def assert_chunks_fast(ctx, ds, ref, what):
+    """assert_chunks for millions of chunks: exact (fsum) sums only where the
+    float64 pairwise sum is not already far inside the bound."""
+    n = len(ds)
+    nb = (n + 63) // 64
+    part, zero = ctx.partials(nb)
+    r = ref[ds.order()]
+    pad = np.full(nb * 64, np.nan)
+    pad[:n] = r
+    seg = pad.reshape(nb, 64)
+    real = ~np.isnan(seg)
+    fin = np.isfinite(seg)
+    nz = (np.isneginf(seg) & real).sum(axis=1)
+    assert np.array_equal(zero & 0xFFFF, nz), what
+    vals = np.where(fin, seg, 0.0)
+    want = vals.sum(axis=1)
+    scale = np.abs(vals).sum(axis=1)
+    err = np.abs(part - want)
+    bound = 1e-12 * scale + 1e-12
+    # numpy's float64 row sums are within ~64 ulp of scale of the exact sum:
+    # recheck with fsum wherever that could matter
+    close = err > 0.5 * bound
+    for c in np.flatnonzero(close):
+        w = math.fsum(vals[c])
+        assert abs(part[c] - w) <= bound[c], (what, c, part[c], w, scale[c])
+    return int(close.sum())
 
 
 def _ctx_with(env):
@@ -209,10 +261,32 @@ def lean_ctx(gpu):
     ctx.close()
 
 
+def one_launch_path(args):
+    """The kernels of a predicted level-0-only call of <= 256 trials: the
+    one-block launch (small_kernel; the full DDM's small_split_kernel)."""
+    sz, st = args[4], args[6]
+    if sz == 0 and st == 0:
+        return {"small", "direct"}
+    if sz > 0 and st > 0:
+        return {"small", "lean", "small_split"}
+    return {"small", "lean"}
+
+
+def check_one_launch(path, args, n, what):
+    """A node-sized call that neither refined nor deferred took the one-block
+    kernel of its family (not level 0 + a separate finalize)."""
+    names = path_names(path)
+    if n <= 256 and not names & {"engine", "redo", "fold"}:
+        assert names == one_launch_path(args), (what, names)
+        return True
+    return False
+
+
 def _both_contexts(gpu, lean_ctx, x, args, what, oracle_lib, need):
     """Per trial and per chunk on the default context's predicted path and on
     the forced-lean one (which must include a kernel of `need`); the two
-    totals are bitwise equal."""
+    totals are bitwise equal. A predicted level-0-only call of <= 256 trials
+    must be the one-block launch of its family."""
     from hddm_amd import _lib
     ref = ref_terms(oracle_lib, x, args)
     tots = []
@@ -220,6 +294,7 @@ def _both_contexts(gpu, lean_ctx, x, args, what, oracle_lib, need):
         ds = gpu.Dataset(x, ctx=ctx)
         ds.wiener_like(*args, *KN)
         tot, terms, path = summing_vs_trials(ctx, ds, args)
+        check_one_launch(path, args, len(x), what)
         if ctx is lean_ctx:
             assert path_names(path) & need, (what, path_names(path))
         assert_terms(terms, ref, f"{what} {path_names(path)}")
@@ -258,6 +333,40 @@ def test_node_sized_one_launch_per_trial(gpu, oracle_lib, lean_ctx, n):
         # is never predicted level-0-only, so small_kernel is not taken)
         _both_contexts(gpu, lean_ctx, x, args, f"node-sized {n} {args}", oracle_lib,
                        {"small", "lean"})
+
+
+NODE_FAMILIES = (SIMPLE, PINNED, (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.1),
+                 (0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 17, 64, 65, 200, 250, 256])
+def test_node_sized_calls_take_the_one_block_kernel(gpu, oracle_lib, n):
+    """What an install()ed HDDM node call runs (hddm/likelihoods.py:52-55 per
+    node): data on which no trial refines (the oracle's evaluation count is
+    the root level's, so the reference's trees stop at level 0) is predicted
+    level-0-only after one call, and that call must be ONE launch of the
+    family's one-block kernel: small_kernel (direct / 1-D families) or
+    small_split_kernel (the full DDM). A regression back to level 0 + a
+    separate finalize fails here. Per trial and per chunk against the
+    reference on the same calls."""
+    from hddm_amd import _lib
+    rng = np.random.default_rng(5000 + n)
+    x = rng.choice([-1.0, 1.0], n) * (0.5 + rng.gamma(2.0, 0.3, n))
+    ctx = _lib.context()
+    for args in NODE_FAMILIES:
+        root = 1 if (args[4] == 0 and args[6] == 0) else (25 if args[4] > 0 and args[6] > 0 else 5)
+        assert oracle_lib.count_evals(x, *args, *KN[:5]) == n * root, "data refines"
+        ref = ref_terms(oracle_lib, x, args)
+        ds = gpu.Dataset(x, ctx=ctx)
+        ds.wiener_like(*args, *KN)
+        tot, terms, path = summing_vs_trials(ctx, ds, args)
+        assert path_names(path) == one_launch_path(args), (n, args, path_names(path))
+        assert_terms(terms, ref, f"one-block {n} {args}")
+        assert_chunks(ctx, ds, ref, f"one-block {n} {args}")
+        assert ds.wiener_like(*args, *KN) == tot
+        assert path_names(ctx.last_path()) == one_launch_path(args)
+        ds.close()
 
 
 def _seed3():

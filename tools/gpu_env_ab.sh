@@ -13,7 +13,7 @@ if [ "${TESTS:-1}" = 1 ]; then
 fi
 for r in $(seq 1 $REPS); do
   for val in $A $B; do
-    env $VAR=$val timeout -k 10 200 python bench.py --steps 50 --warmup 5 --no-cpu-baseline > $O/bench_${val}_$r.log 2>&1 || { echo "BENCH_FAIL $val rc=$?"; tail -5 $O/bench_${val}_$r.log; exit 1; }
+    env $VAR=$val timeout -k 10 200 python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-stress > $O/bench_${val}_$r.log 2>&1 || { echo "BENCH_FAIL $val rc=$?"; tail -5 $O/bench_${val}_$r.log; exit 1; }
     python - $O/bench_${val}_$r.log $VAR=$val <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

@@ -9,7 +9,7 @@ rm -rf $OUT/trace $OUT/fetch $OUT/write $OUT/sq $OUT/f64
 # the source digest of the library these passes measure (summarize_profile.py
 # ties the summary to it)
 cp hddm_amd/lib/libwfpt_amd.so.src $OUT/src_sha1.txt
-B="python3 bench.py --steps ${STEPS:-20} --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-}"
+B="python3 bench.py --steps ${STEPS:-20} --warmup 2 --no-cpu-baseline --no-stress ${BENCH_ARGS:-}"
 timeout -k 10 300 python3 bench.py --steps 30 --warmup 3 --cpu-seconds 10 > $OUT/bench_plain.log 2>&1 || { echo "BENCH_FAIL rc=$?"; exit 1; }
 echo bench-ok
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true

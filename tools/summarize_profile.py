@@ -48,6 +48,10 @@ def main():
     ap.add_argument("--name", default="pmc_summary", help="summary file name under profiles/<tag>/")
     ap.add_argument("--no-traffic", action="store_true",
                     help="do not write profiles/traffic.json (secondary kernels)")
+    ap.add_argument("--traffic-out", default="traffic.json",
+                    help="file under profiles/ for the digest-matched figures bench.py reads "
+                         "(traffic.json: the headline kernel; traffic_stress.json: the engine "
+                         "on the stress sets)")
     a = ap.parse_args()
     prof = a.prof_dir
     out_dir = os.path.join(ROOT, "profiles", a.tag)
@@ -96,8 +100,8 @@ def main():
     if a.no_traffic:
         print(json.dumps(summary, indent=1))
         return
-    with open(os.path.join(ROOT, "profiles", "traffic.json"), "w") as fh:
-        json.dump({"src_sha1": sha, "source": f"profiles/{a.tag}/pmc_summary.json", "kernel": a.kernel,
+    with open(os.path.join(ROOT, "profiles", a.traffic_out), "w") as fh:
+        json.dump({"src_sha1": sha, "source": f"profiles/{a.tag}/{a.name}.json", "kernel": a.kernel,
                    "n_trials": a.trials, "hbm_bytes_per_launch": fetch_b + write_b,
                    "hbm_bytes_per_trial": (fetch_b + write_b) / a.trials,
                    "valu_issue_utilisation": summary["valu_issue_utilisation"],
