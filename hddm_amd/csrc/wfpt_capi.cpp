@@ -148,6 +148,11 @@ struct wfpt_ctx {
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
   DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
+  DevBuf<wfpt::Params> nd_row;     // wiener_like_nodes: device copy of the call's node rows
+  DevBuf<wfpt::NodeGrid> nd_grid;  // ... and each node's root z grids + sine tables (split pass)
+  int* ncnt = nullptr;       // device [4]: the node path's listed chunks / records counters and
+                             // [3] the publish ticket (0 at rest: the call's last kernel resets
+                             // them; a failed call restores them)
   int* n_defer = nullptr;    // device [4]: the per-node path's listed chunks, chunk-path records,
                              // fast-pass records (0 at rest)
   unsigned long long* evals = nullptr;
@@ -160,6 +165,7 @@ struct wfpt_ctx {
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
+  bool node_split = true;      // WFPT_NODE_SPLIT=0: the per-node level 0 one lane per trial
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
   bool small = true;           // WFPT_SMALL=0: one-block calls keep the separate finalize
@@ -638,6 +644,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   c->device = device;
   if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
+  if (const char* ns = std::getenv("WFPT_NODE_SPLIT")) c->node_split = std::strcmp(ns, "0") != 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
   if (const char* sm = std::getenv("WFPT_SMALL")) c->small = std::strcmp(sm, "0") != 0;
@@ -655,6 +662,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipHostGetDevicePointer((void**)&c->mres_dev, c->mres, 0);
   if (e == hipSuccess) e = hipMalloc((void**)&c->n_defer, 4 * sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->n_defer, 0, 4 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->ncnt, 4 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(c->ncnt, 0, 4 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
@@ -706,6 +715,9 @@ void wfpt_close(wfpt_ctx* c) {
   c->nd_par.release();
   c->nd_chunks.release();
   if (c->n_defer) (void)hipFree(c->n_defer);
+  if (c->ncnt) (void)hipFree(c->ncnt);
+  c->nd_row.release();
+  c->nd_grid.release();
   if (c->tree_any) (void)hipFree(c->tree_any);
   if (c->fin) (void)hipFree(c->fin);
   if (c->fin_ticket) (void)hipFree(c->fin_ticket);
@@ -1034,18 +1046,34 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
     HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
     HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>((d->n + 63) / 64, 1)));
-    HIP_TRY(hipMemsetAsync(c->n_defer, 0, 3 * sizeof(int), c->stream));
   }
+  // the split level 0 (adaptive t families, non-counting calls): the call's
+  // node rows + root z grids in device memory
+  const bool split = (mode == wfpt::kAdaptT || mode == wfpt::kAdaptTZ) && !c->count && c->node_split;
+  if (split) {
+    HIP_TRY(c->nd_row.reserve(std::max<int32_t>(m, 1)));
+    HIP_TRY(c->nd_grid.reserve(2 * (size_t)std::max<int32_t>(m, 1)));
+  }
+  const wfpt::NodeTables nt{c->nd_row.p, c->nd_grid.p, m};
+  c->path = split ? WFPT_PATH_NODE_SPLIT : 0;
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, mode, c->lp.p, c->nd_idx.p,
-                     c->nd_par.p, c->n_defer, c->nd_chunks.p, c->count ? c->evals : nullptr,
-                     c->status, c->prof, c->stream);
+                     c->nd_par.p, c->ncnt, c->nd_chunks.p, c->count ? c->evals : nullptr,
+                     c->status, c->prof, c->stream, split ? &nt : nullptr);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   return WFPT_OK;
+}
+
+// A node call that failed after its kernels were enqueued: the node counters
+// (0 at rest, reset by the call's last kernel) may be left set; restore them.
+int nodes_recover(wfpt_ctx* c, int rc) {
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipMemset(c->ncnt, 0, 4 * sizeof(int));
+  return rc;
 }
 
 int nodes_check(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node, const wfpt_knobs* k,
@@ -1067,14 +1095,16 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
-  if (int rc = nodes_launch(c, d, per_node, K)) return rc;
+  if (int rc = nodes_launch(c, d, per_node, K)) return nodes_recover(c, rc);
   ++c->seq;
   if (m > 0) {
     // per-node sums, status and the completion word land in mapped memory
+    // (one launch; its last block resets the node counters)
     wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->mnode.d, c->status, c->seq,
-                             c->stream);
-    HIP_TRY(hipGetLastError());
-    if (int rc = wait_word(c, c->mnode.h + m + 1)) return rc;
+                             c->stream, c->ncnt + 3, c->ncnt);
+    if (hipGetLastError() != hipSuccess)
+      return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_publish_kernel launch failed"));
+    if (int rc = wait_word(c, c->mnode.h + m + 1)) return nodes_recover(c, rc);
     if (int rc = check_status_value(c->mnode.h[m])) return rc;
   } else {
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1095,8 +1125,8 @@ int wfpt_wiener_like_nodes_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_param
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
-  if (int rc = nodes_launch(c, d, per_node, K)) return rc;
-  wfpt::launch_segment_res(c->lp.p, d->off, m, c->res.p, c->status, false, c->stream);
+  if (int rc = nodes_launch(c, d, per_node, K)) return nodes_recover(c, rc);
+  wfpt::launch_segment_res(c->lp.p, d->off, m, c->res.p, c->status, false, c->stream, c->ncnt);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(out, c->res.p, ((size_t)m + 1) * sizeof(double), hipMemcpyDeviceToHost,
                          c->stream));
@@ -1140,7 +1170,7 @@ int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_p
     }
   }
   wfpt::launch_segment_res(lrc == WFPT_OK ? c->lp.p : nullptr, lrc == WFPT_OK ? d->off : nullptr,
-                           m, c->res.p, c->status, lrc != WFPT_OK, c->stream);
+                           m, c->res.p, c->status, lrc != WFPT_OK, c->stream, c->ncnt);
   if (hipGetLastError() != hipSuccess) {
     (void)ncclCommAbort(c->comm);
     c->comm = nullptr;

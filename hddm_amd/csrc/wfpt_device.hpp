@@ -1952,6 +1952,17 @@ __host__ __device__ inline void root_grids(const Params& P, RootGrids& R) {
   }
 }
 
+// Per-call node tables of the split per-node level-0 pass (wfpt_kernels.hip:
+// node_grid_kernel / node_split_kernel): for node j and boundary flip, entry
+// 2 j + flip holds the root z grid and its large-time sine table -- the
+// zgrid_of / sin_table calls of root_grids with the node's parameters, i.e.
+// the grid the per-lane level 0 builds (zgrid_setup of the same bounds) and
+// the sines its recurrence produces, bit for bit.
+struct NodeGrid {
+  ZGrid G;
+  double S[kSinK + 1][5];
+};
+
 // P(hit upper boundary), pdf.pxi:67-72
 __device__ inline double prob_ub(double v, double a, double z) {
   if (v == 0) return z;

@@ -126,22 +126,36 @@ void launch_poison(double* res, hipStream_t s);
 // unused), or -1 (mixed /
 // fixed Simpson: one generic per-trial kernel with a per-lane mode). prof
 // (COUNT builds, evals != null): the node tallies of wfpt_profile_lists.
+// nt (optional): the call's node tables (device); with them the adaptive t
+// families (kAdaptT, kAdaptTZ) of a non-counting call run node_grid_kernel +
+// node_split_kernel (five lanes per trial) instead of node_fast_kernel.
+struct NodeGrid;
+struct NodeTables {
+  Params* prow;     // [n_nodes] device copy of the call's rows
+  NodeGrid* ngrid;  // [2 n_nodes] root z grid + sine table per node and boundary
+  int32_t n_nodes;
+};
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
                   int* n_defer, int* clist, unsigned long long* evals, int* status, int* prof,
-                  hipStream_t s);
+                  hipStream_t s, const NodeTables* nt = nullptr);
 // res (device, n_nodes) per-node sums; then out (mapped host): [0, n_nodes)
 // the sums, [n_nodes] encoded error flags, [n_nodes + 1] the completion word.
 // Node all-reduce: res[0, n_nodes) per-node sums (or zeros when poison),
 // res[n_nodes] the encoded error count (kPeerFailUnit when poison; the device
 // status word is reset); then, after the exchange, res -> out[0, n_nodes] and
 // the completion word out[n_nodes + 1].
+// counters: the node path's n_defer words, reset to 0 (0 at rest)
 void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
-                        int* status, bool poison, hipStream_t s);
+                        int* status, bool poison, hipStream_t s, int* counters);
 void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long long seq,
                         hipStream_t s);
+// One launch (segment_publish_kernel): the per-node sums into res, then the
+// last block (ticket, 0 at rest) publishes them to out with the error word
+// and the completion word and resets counters[0..2] (0 at rest).
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
-                        double* out, int* status, unsigned long long seq, hipStream_t s);
+                        double* out, int* status, unsigned long long seq, hipStream_t s,
+                        int* ticket, int* counters);
 // wiener_like_multi with a uniform adaptive / direct family (mode): level-0
 // pass + deferred trials (d_idx / d_par hold up to n records, *n_defer must
 // be 0 on the stream) into lp[n], then per-block sums into part / zeros

@@ -1572,12 +1572,71 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
   }
 }
 
+// segment_sum_kernel's per-node sums and publish_nodes_kernel's publication in
+// one launch: each wave writes its node's sum to res (agent-scope release),
+// and the last block to finish (agent-scope ticket) copies the n sums to the
+// mapped slot, then the encoded error flags and the completion word, and
+// resets the call's counters (the node path's n_defer words and the ticket:
+// 0 at rest for the next call, stream order).
+__global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, const int64_t* off,
+                                                              int32_t n_nodes, double* res,
+                                                              int* status, double* out,
+                                                              unsigned long long seq, int* ticket,
+                                                              int* counters) {
+  __shared__ int last;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j < n_nodes) {
+    const int64_t lo = off[j], hi = off[j + 1];
+    double s = 0.0;
+    int zero = 0;
+    for (int64_t i = lo + lane; i < hi; i += 64) {
+      const double v = lp[i];
+      if (v == -INFINITY) zero = 1;
+      else s += v;
+    }
+    s = wave_sum(s);
+    const bool anyz = __ballot(zero != 0) != 0ull;
+    if (lane == 0) {
+      res[j] = anyz ? -INFINITY : s;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int k = threadIdx.x; k < n_nodes; k += 256)
+    out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *ticket = 0;
+    counters[0] = 0;
+    counters[1] = 0;
+    counters[2] = 0;
+    const int st = atomicExch(status, 0);
+    out[n_nodes] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+    __threadfence_system();
+    reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
+    __threadfence_system();
+  }
+}
+
 // Node all-reduce (wfpt_wiener_like_nodes_allreduce): the encoded error
 // count of this rank's node pass appended to its per-node sums (res[n]),
 // status reset; or a failed rank's poisoned vector {0 ..., kPeerFailUnit}.
 __global__ __launch_bounds__(64) void node_status_kernel(double* res, int32_t n, int* status,
-                                                         int poison) {
+                                                         int poison, int* counters) {
   if (threadIdx.x == 0) {
+    counters[0] = 0;  // the node path's n_defer words: 0 at rest
+    counters[1] = 0;
+    counters[2] = 0;
     const int st = atomicExch(status, 0);
     res[n] = poison ? kPeerFailUnit
                     : (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
@@ -1724,6 +1783,96 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
     if (lane == 0) {
       atomicAdd(evals, (unsigned long long)ne);
       if (b) atomicAdd(&prof[3], __popcll(b));
+    }
+  }
+}
+
+// Split per-node level 0 (the adaptive t families: kAdaptT, kAdaptTZ -- the
+// full DDM of config 4). A batched node call of ~100k trials is ~1.5k waves:
+// fewer than the chip's SIMDs, so node_fast_kernel's one-lane-per-trial level
+// 0 lasts one wave's latency (25 dependent evaluations per lane). Here block c
+// takes chunk c (64 stored trials) with kNodeSplit = 5 waves: wave j evaluates
+// t node j of all 64 trials (l0_node: the function of the per-lane loop and of
+// the split units, bit-identical to it; j is wave-uniform), on the trial's
+// node row and root z grid + sine table from the call's node tables
+// (node_grid_kernel). Then wave 0 takes one trial per lane again: the root
+// stop test and value from the five node values (l0_finish, as
+// small_split_kernel), the term, and -- exactly as node_fast_kernel -- a chunk
+// with a trial that refines or needs the exact path is listed for
+// node_chunk_kernel with its deferred trials as records.
+constexpr int kNodeSplit = 5;
+__global__ __launch_bounds__(256) void node_grid_kernel(const Params* P, int32_t n_nodes,
+                                                        Params* prow, NodeGrid* ng, int grids) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= 2 * n_nodes) return;
+  const int j = k >> 1, flip = k & 1;
+  const Params Q = P[j];  // the mapped table the host filled for this call
+  if (flip == 0) prow[j] = Q;
+  if (!grids) return;
+  const double zf = flip ? 1. - Q.z : Q.z, vf = flip ? -Q.v : Q.v;
+  const ZGrid G = zgrid_of(zf - Q.sz / 2., zf + Q.sz / 2., kGridRoot, vf, Q.sv, Q.a);
+  ng[k].G = G;
+  sin_table(G, ng[k].S);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kNodeSplit * 64) void node_split_kernel(
+    const double* x, const int32_t* node, int64_t n, const Params* prow, const NodeGrid* ng,
+    Knobs K, double* lp, int64_t* d_idx, Params* d_par, int* clist, int* n_chunks) {
+  static_assert(MODE == kAdaptT || MODE == kAdaptTZ, "t-node split");
+  __shared__ double sf[kNodeSplit][64];
+  __shared__ int sfl[kNodeSplit][64];
+  __shared__ int spd[kNodeSplit][64];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t c = blockIdx.x;
+  const int64_t i = c * 64 + lane;
+  const bool own = i < n;
+  const double x0 = own ? x[i] : 0.0;
+  const int nj = own ? node[i] : 0;
+  const Params Q = prow[nj];
+  const Trial tr = trial_setup(x0, Q);
+  double y = 0.0;
+  int flags = 0;
+  bool pj = false;
+  if (own && tr.valid) {
+    double lb, ub;
+    tree_root<MODE>(tr, Q, lb, ub);
+    const L0Hints H = l0_hints(tr.x, lb, ub, Q.a, K.err);
+    long long ne = 0;
+    const NodeGrid& g = ng[2 * nj + (x0 > 0 ? 1 : 0)];
+    y = l0_node<MODE>(tr, Q, K, lb, ub, H, wv, g.G, flags, pj, ne,
+                      MODE == kAdaptTZ ? &g.S[0][0] : nullptr);
+  }
+  sf[wv][lane] = y;
+  sfl[wv][lane] = flags;
+  spd[wv][lane] = pj ? 1 : 0;
+  __syncthreads();
+  if (wv != 0) return;
+  int fl = 0;
+  unsigned pd = 0u;
+#pragma unroll
+  for (int q = 0; q < kNodeSplit; ++q) {
+    fl |= sfl[q][lane];
+    if (spd[q][lane]) pd |= 1u << (q * (kTreeW / 4));
+  }
+  const double f[5] = {sf[0][lane], sf[1][lane], sf[2][lane], sf[3][lane], sf[4][lane]};
+  double p = 0.0;
+  int oc = kFinal;
+  if (own) oc = l0_finish<MODE>(tr, Q, K, fl, pd, f, p);
+  const bool defer = own && oc != kFinal;
+  if (own && !defer) lp[i] = node_logp(p, Q, K);
+  const unsigned long long b = __ballot(defer);
+  if (b) {  // node_fast_kernel's listing: the chunk, and its deferred trials as records
+    int base = 0;
+    if (lane == 0) {
+      clist[atomicAdd(n_chunks, 1)] = (int)c;
+      base = atomicAdd(n_chunks + 2, __popcll(b));
+    }
+    base = __shfl(base, 0, 64);
+    if (defer) {
+      const int k = base + __popcll(b & lanemask_lt(lane));
+      d_idx[k] = i;
+      d_par[k] = Q;
     }
   }
 }
@@ -2208,10 +2357,24 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                                   const Params* P, const Knobs& K, double* lp, int64_t* d_idx,
                                   Params* d_par, int* n_defer, int* clist,
                                   unsigned long long* evals, int* status, int* prof,
-                                  hipStream_t s) {
-  hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
-                     node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
-                     prof);
+                                  hipStream_t s, const NodeTables* nt) {
+  bool split = false;
+  if constexpr ((MODE == kAdaptT || MODE == kAdaptTZ) && !COUNT) {
+    if (nt && nt->n_nodes > 0) {
+      // the call's node tables, then the t-node split level 0; the chunk
+      // engine / records below read the device copy of the rows
+      hipLaunchKernelGGL(node_grid_kernel, dim3((2 * nt->n_nodes + 255) / 256), dim3(256), 0, s,
+                         P, nt->n_nodes, nt->prow, nt->ngrid, MODE == kAdaptTZ ? 1 : 0);
+      hipLaunchKernelGGL((node_split_kernel<MODE>), dim3((n + 63) / 64), dim3(kNodeSplit * 64), 0,
+                         s, x, node, n, nt->prow, nt->ngrid, K, lp, d_idx, d_par, clist, n_defer);
+      P = nt->prow;
+      split = true;
+    }
+  }
+  if (!split)
+    hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
+                       node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
+                       prof);
   if constexpr (MODE != kDirect) {
     // adaptive families, one launch: the fast pass's records one wave each
     // when they are sparse in their chunks, else one wave per listed chunk
@@ -2233,10 +2396,11 @@ template <bool COUNT>
 static void launch_nodes_mode(int mode, const double* x, const int32_t* node, int64_t n,
                               const Params* P, const Knobs& K, double* lp, int64_t* d_idx,
                               Params* d_par, int* n_defer, int* clist,
-                              unsigned long long* evals, int* status, int* prof, hipStream_t s) {
+                              unsigned long long* evals, int* status, int* prof, hipStream_t s,
+                              const NodeTables* nt) {
 #define TWO_PASS(M_)                                                                           \
   launch_nodes_two_pass<M_, COUNT>(x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, evals,  \
-                                   status, prof, s)
+                                   status, prof, s, nt)
   switch (mode) {
     case kDirect: TWO_PASS(kDirect); break;
     case kAdaptT: TWO_PASS(kAdaptT); break;
@@ -2249,16 +2413,16 @@ static void launch_nodes_mode(int mode, const double* x, const int32_t* node, in
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
                   int* n_defer, int* clist, unsigned long long* evals, int* status, int* prof,
-                  hipStream_t s) {
+                  hipStream_t s, const NodeTables* nt) {
   const int64_t nb = blocks_for(n);
   if (nb == 0) return;
   if (mode >= kDirect && mode <= kAdaptTZ) {
     if (evals)
       launch_nodes_mode<true>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, evals,
-                              status, prof, s);
+                              status, prof, s, nt);
     else
       launch_nodes_mode<false>(mode, x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, evals,
-                               status, prof, s);
+                               status, prof, s, nt);
     return;
   }
   const int stk = stack_kind(K);
@@ -2278,7 +2442,7 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
 }
 
 void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
-                        int* status, bool poison, hipStream_t s) {
+                        int* status, bool poison, hipStream_t s, int* counters) {
   if (poison) {
     hipLaunchKernelGGL(node_poison_kernel, dim3(std::max<int32_t>((n_nodes + 255) / 256, 1)),
                        dim3(256), 0, s, res, n_nodes);
@@ -2287,7 +2451,7 @@ void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, d
                        n_nodes, res);
   }
   hipLaunchKernelGGL(node_status_kernel, dim3(1), dim3(64), 0, s, res, n_nodes, status,
-                     poison ? 1 : 0);
+                     poison ? 1 : 0, counters);
 }
 
 void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long long seq,
@@ -2296,12 +2460,11 @@ void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long
 }
 
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
-                        double* out, int* status, unsigned long long seq, hipStream_t s) {
+                        double* out, int* status, unsigned long long seq, hipStream_t s,
+                        int* ticket, int* counters) {
   if (n_nodes <= 0) return;
-  hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                     n_nodes, res);
-  hipLaunchKernelGGL(publish_nodes_kernel, dim3(1), dim3(256), 0, s, res, n_nodes, status, out,
-                     seq);
+  hipLaunchKernelGGL(segment_publish_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
+                     n_nodes, res, status, out, seq, ticket, counters);
 }
 
 template <int MODE, bool COUNT>

@@ -287,6 +287,8 @@ int wfpt_debug_partials(wfpt_ctx *ctx, double *part, int32_t *zero, int64_t n);
 #define WFPT_PATH_SPLIT 128  /* heavy chunks split into one-wave units */
 #define WFPT_PATH_SMALL_SPLIT 256 /* the full DDM's one-block call, three lanes per
                                      trial (small_split_kernel; with WFPT_PATH_SMALL) */
+#define WFPT_PATH_NODE_SPLIT 512  /* per-node call: t-node split level 0
+                                     (node_grid_kernel + node_split_kernel) */
 int wfpt_last_path(wfpt_ctx *ctx, int *path);
 int wfpt_synchronize(wfpt_ctx *ctx);
 

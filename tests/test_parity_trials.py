@@ -99,6 +99,62 @@ def test_node_terms_per_trial(gpu, oracle_lib, family):
     assert np.array_equal(ds.wiener_like_nodes(P, *KN), sums, equal_nan=True)
 
 
+@pytest.fixture(scope="module")
+def one_lane_ctx(gpu):
+    """A context whose per-node level 0 runs one lane per trial
+    (node_fast_kernel; WFPT_NODE_SPLIT=0), the reference point of the split."""
+    import os
+    from hddm_amd import _lib
+    old = os.environ.get("WFPT_NODE_SPLIT")
+    os.environ["WFPT_NODE_SPLIT"] = "0"
+    try:
+        ctx = _lib.Context(0)
+    finally:
+        if old is None:
+            del os.environ["WFPT_NODE_SPLIT"]
+        else:
+            os.environ["WFPT_NODE_SPLIT"] = old
+    yield ctx
+    ctx.close()
+
+
+@pytest.mark.parametrize("family", ["full", "heavy", "st_only", "c4_full"])
+def test_node_split_level0_bit_identical(gpu, oracle_lib, one_lane_ctx, family):
+    """The t-node split level 0 of the batched node call (node_grid_kernel +
+    node_split_kernel: five lanes per trial, the node tables built once per
+    call) gives every trial the bits of the one-lane-per-trial pass
+    (node_fast_kernel), per trial and per node, and it is the path the
+    default context takes (WFPT_PATH_NODE_SPLIT); per trial against the
+    reference at 1e-6."""
+    from hddm_amd import _lib
+    if family == "c4_full":
+        from hddm_amd.hierarchical import HDDM, gen_data
+        data, _ = gen_data(n_subj=200, n_trials=500, sv=0.1, sz=0.1, st=0.1)
+        m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st"), p_outlier=0.05)
+        x = data["rt"].to_numpy(dtype=np.float64)
+        node = data.groupby(["subj_idx", "cond"], sort=True).ngroup().to_numpy()
+        P = m.node_table()
+        kn = (m.wp["err"], m.wp["n_st"], m.wp["n_sz"], m.wp["use_adaptive"], m.wp["simps_err"],
+              m.wp["w_outlier"])
+    else:
+        rng = np.random.default_rng({"full": 11, "heavy": 12, "st_only": 13}[family])
+        x, node, P = _node_dataset(rng, 57, family)
+        kn = KN
+    out = []
+    for ctx in (_lib.context(), one_lane_ctx):
+        ds = gpu.Dataset(x, node_id=node, n_nodes=P.shape[0], ctx=ctx)
+        sums, terms = ds.wiener_like_nodes(P, *kn, trials=True)
+        split = bool(ctx.last_path() & _lib.PATH_NODE_SPLIT)
+        assert split == (ctx is not one_lane_ctx), family
+        assert np.array_equal(ds.wiener_like_nodes(P, *kn), sums, equal_nan=True)
+        out.append((sums, terms))
+        ds.close()
+    assert np.array_equal(out[0][1], out[1][1], equal_nan=True), family
+    assert np.array_equal(out[0][0], out[1][0], equal_nan=True), family
+    ref = node_terms_ref(oracle_lib, x, node, P, kn)
+    assert_logp_parity(out[0][1], ref, f"split {family}")
+
+
 @pytest.mark.parametrize("case", ["adapt_tz", "direct", "adapt_t", "adapt_z", "generic_sz",
                                   "heavy"])
 def test_multi_terms_per_trial(gpu, oracle_lib, case):
