@@ -149,7 +149,7 @@ struct wfpt_ctx {
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
   DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
   DevBuf<wfpt::Params> nd_row;     // wiener_like_nodes: device copy of the call's node rows
-  DevBuf<wfpt::NodeGrid> nd_grid;  // ... and each node's root z grids + sine tables (split pass)
+  DevBuf<wfpt::EngTables> nd_etab; // ... and each node's engine tables (speculative records)
   int* ncnt = nullptr;       // device [4]: the node path's listed chunks / records counters and
                              // [3] the publish ticket (0 at rest: the call's last kernel resets
                              // them; a failed call restores them)
@@ -717,7 +717,7 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->n_defer) (void)hipFree(c->n_defer);
   if (c->ncnt) (void)hipFree(c->ncnt);
   c->nd_row.release();
-  c->nd_grid.release();
+  c->nd_etab.release();
   if (c->tree_any) (void)hipFree(c->tree_any);
   if (c->fin) (void)hipFree(c->fin);
   if (c->fin_ticket) (void)hipFree(c->fin_ticket);
@@ -1052,9 +1052,9 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
   const bool split = (mode == wfpt::kAdaptT || mode == wfpt::kAdaptTZ) && !c->count && c->node_split;
   if (split) {
     HIP_TRY(c->nd_row.reserve(std::max<int32_t>(m, 1)));
-    HIP_TRY(c->nd_grid.reserve(2 * (size_t)std::max<int32_t>(m, 1)));
+    HIP_TRY(c->nd_etab.reserve(std::max<int32_t>(m, 1)));
   }
-  const wfpt::NodeTables nt{c->nd_row.p, c->nd_grid.p, m};
+  const wfpt::NodeTables nt{c->nd_row.p, c->nd_etab.p, m};
   c->path = split ? WFPT_PATH_NODE_SPLIT : 0;
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));

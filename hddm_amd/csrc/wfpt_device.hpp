@@ -1872,12 +1872,16 @@ __host__ __device__ inline ZGrid zgrid_of(double lb, double ub, int sel, double 
 // values below lv; otherwise need = the refining intervals of level lv
 // (bit m: interval m of that level), and for lv == kTreeDepth those mean a
 // deeper tree. flags gets kFlagExact for a stop test inside kTieBand; nref =
-// visited refined intervals (2 new nodes x 2 evaluations each).
+// visited refined intervals (2 new nodes x 2 evaluations each). used
+// (optional): bit k set for every point f[k] the recursion read (the points
+// the reference evaluates).
 __host__ __device__ inline double tree17(const double (&f)[kTreePoints],
                                          const double (&P)[kTreePoints], double err, int depth,
-                                         int lv, int& flags, unsigned& need, int& nref) {
+                                         int lv, int& flags, unsigned& need, int& nref,
+                                         unsigned* used = nullptr) {
   need = 0u;
   nref = 0;
+  if (used) *used = 0x11111u;  // points 0, 4, 8, 12, 16
   const double h0 = P[kTreeW] - P[0];
   const double S0 = (h0 / 6) * ((f[0] + (4 * f[8])) + f[16]);
   const Simp r = simp5(h0, f[0], f[4], f[8], f[12], f[16]);
@@ -1888,6 +1892,7 @@ __host__ __device__ inline double tree17(const double (&f)[kTreePoints],
     return 0.0;
   }
   double vh[2];
+  if (used) *used |= 0x4444u;  // the halves' aux points 2, 6, 10, 14
 #pragma unroll
   for (int m = 0; m < 2; ++m) {
     const int lo = 8 * m;
@@ -1903,6 +1908,7 @@ __host__ __device__ inline double tree17(const double (&f)[kTreePoints],
       vh[m] = 0.0;
       continue;
     }
+    if (used) *used |= 0xAAu << lo;  // the half's quarter aux points lo + 1, 3, 5, 7
     double vq[2];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -1951,17 +1957,6 @@ __host__ __device__ inline void root_grids(const Params& P, RootGrids& R) {
     sin_table(R.G[flip], R.S[flip]);
   }
 }
-
-// Per-call node tables of the split per-node level-0 pass (wfpt_kernels.hip:
-// node_grid_kernel / node_split_kernel): for node j and boundary flip, entry
-// 2 j + flip holds the root z grid and its large-time sine table -- the
-// zgrid_of / sin_table calls of root_grids with the node's parameters, i.e.
-// the grid the per-lane level 0 builds (zgrid_setup of the same bounds) and
-// the sines its recurrence produces, bit for bit.
-struct NodeGrid {
-  ZGrid G;
-  double S[kSinK + 1][5];
-};
 
 // P(hit upper boundary), pdf.pxi:67-72
 __device__ inline double prob_ub(double v, double a, double z) {

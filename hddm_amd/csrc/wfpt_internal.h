@@ -129,10 +129,11 @@ void launch_poison(double* res, hipStream_t s);
 // nt (optional): the call's node tables (device); with them the adaptive t
 // families (kAdaptT, kAdaptTZ) of a non-counting call run node_grid_kernel +
 // node_split_kernel (five lanes per trial) instead of node_fast_kernel.
-struct NodeGrid;
+struct EngTables;
 struct NodeTables {
   Params* prow;     // [n_nodes] device copy of the call's rows
-  NodeGrid* ngrid;  // [2 n_nodes] root z grid + sine table per node and boundary
+  EngTables* etab;  // [n_nodes] each node's engine tables (root grids: the split
+                    // level 0; all of it: the speculative records)
   int32_t n_nodes;
 };
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,

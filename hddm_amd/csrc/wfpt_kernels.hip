@@ -1801,23 +1801,37 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
 // with a trial that refines or needs the exact path is listed for
 // node_chunk_kernel with its deferred trials as records.
 constexpr int kNodeSplit = 5;
+// One thread per (node j, boundary flip, z grid sel): node j's EngTables in
+// et[j] (eng_tables' z grids, dyadic points and 1 / (ub_z - lb_z), by the same
+// functions: the root grids are what the split level 0 reads, all of it what
+// the speculative records read) and the device copy of its row. grids = 0
+// (kAdaptT): rows and t points only.
 __global__ __launch_bounds__(256) void node_grid_kernel(const Params* P, int32_t n_nodes,
-                                                        Params* prow, NodeGrid* ng, int grids) {
+                                                        Params* prow, EngTables* et, int grids) {
   const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= 2 * n_nodes) return;
-  const int j = k >> 1, flip = k & 1;
+  if (k >= 8 * n_nodes) return;
+  const int j = k >> 3, flip = (k >> 2) & 1, sel = k & 3;
   const Params Q = P[j];  // the mapped table the host filled for this call
-  if (flip == 0) prow[j] = Q;
+  EngTables& T = et[j];
+  if (flip == 0 && sel == 0) {
+    prow[j] = Q;
+    for (int q = 0; q < kTreePoints; ++q)
+      T.tP[q] = dyadic_point(Q.t - Q.st / 2., Q.t + Q.st / 2., q);
+  }
   if (!grids) return;
   const double zf = flip ? 1. - Q.z : Q.z, vf = flip ? -Q.v : Q.v;
-  const ZGrid G = zgrid_of(zf - Q.sz / 2., zf + Q.sz / 2., kGridRoot, vf, Q.sv, Q.a);
-  ng[k].G = G;
-  sin_table(G, ng[k].S);
+  const double zl = zf - Q.sz / 2., zu = zf + Q.sz / 2.;
+  const ZGrid G = zgrid_of(zl, zu, sel, vf, Q.sv, Q.a);
+  T.G[flip][sel] = G;
+  if (sel == 1) {
+    for (int q = 0; q < kTreePoints; ++q) T.zP[flip][q] = dyadic_point(zl, zu, q);
+    T.iz[flip] = 1.0 / (zu - zl);
+  }
 }
 
 template <int MODE>
 __global__ __launch_bounds__(kNodeSplit * 64) void node_split_kernel(
-    const double* x, const int32_t* node, int64_t n, const Params* prow, const NodeGrid* ng,
+    const double* x, const int32_t* node, int64_t n, const Params* prow, const EngTables* et,
     Knobs K, double* lp, int64_t* d_idx, Params* d_par, int* clist, int* n_chunks) {
   static_assert(MODE == kAdaptT || MODE == kAdaptTZ, "t-node split");
   __shared__ double sf[kNodeSplit][64];
@@ -1839,9 +1853,12 @@ __global__ __launch_bounds__(kNodeSplit * 64) void node_split_kernel(
     tree_root<MODE>(tr, Q, lb, ub);
     const L0Hints H = l0_hints(tr.x, lb, ub, Q.a, K.err);
     long long ne = 0;
-    const NodeGrid& g = ng[2 * nj + (x0 > 0 ? 1 : 0)];
-    y = l0_node<MODE>(tr, Q, K, lb, ub, H, wv, g.G, flags, pj, ne,
-                      MODE == kAdaptTZ ? &g.S[0][0] : nullptr);
+    // the root z grid in registers, loaded once (the large-time sines by the
+    // per-lane recurrence, as node_fast_kernel: a per-lane table would put
+    // dependent vector loads in the series loop)
+    ZGrid G{};
+    if (MODE == kAdaptTZ) G = et[nj].G[x0 > 0 ? 1 : 0][kGridRoot];
+    y = l0_node<MODE>(tr, Q, K, lb, ub, H, wv, G, flags, pj, ne, nullptr);
   }
   sf[wv][lane] = y;
   sfl[wv][lane] = flags;
@@ -1877,6 +1894,153 @@ __global__ __launch_bounds__(kNodeSplit * 64) void node_split_kernel(
   }
 }
 
+// Speculative record (non-counting node calls of the adaptive t families,
+// with the call's node tables): a deferred trial of a sparse call is one
+// wave's work, and the breadth-first rounds (node_records) walk its tree
+// level by level -- six or more dependent rounds of one grid evaluation each.
+// Here the wave evaluates EVERY value the reference's recursion can reach at
+// n_st = n_sz = kTreeDepth in two rounds: the 17 dyadic t points x the 4 z
+// grids (kAdaptTZ; kAdaptT: the 17 t points), plus the level-0 t points' root
+// grids once more with the level-0 hints, exactly as the engine evaluates
+// them (its stage-0 tasks of level 0 take l0_hints, its z walks do not).
+// Then 17 lanes settle each t point's value as the engine's task completion
+// does (the root test, simp_value, or the z walk's tree17 over its 17
+// values), and lane 0 runs tree17 over the t points. Only the points that
+// recursion reads (tree17's `used`) contribute their flags (ambiguous
+// decisions, ties, deeper trees), so the trial's density and its deferral
+// are the engine's; the extra values are never read. LDS: buf (>= 314
+// doubles: the walk values and the hinted root grids), tv (17 t values),
+// pf (>= 39 ints of point flags); lp[i] gets the node term.
+constexpr int kOvfBit = 1 << 8;  // a grid's drift factor overflowed (literal values)
+template <int MODE>
+__device__ inline void node_record_spec(double* buf, double* tv, int* pf, int lane,
+                                        const double* x, const int32_t* node, const Knobs& K,
+                                        double* lp, int64_t i, const Params& Q,
+                                        const EngTables* et, int& errf) {
+  constexpr int NP = kTreePoints;
+  constexpr int NG = MODE == kAdaptTZ ? 4 : 1;  // grids per t point
+  constexpr int NE = NP * NG + (MODE == kAdaptTZ ? 5 : 0);
+  double* zv = buf;             // [NP][NP] the unhinted grids' values (the z walks)
+  double* hv = buf + NP * NP;   // [5][5] the hinted root grids of the level-0 t points
+  int* fu = pf;                 // [NP] unhinted root grid: kFlagExact (ambiguous) | kOvfBit
+  int* fh = pf + NP;            // [5] hinted root grid: the same
+  int* fp = pf + NP + 5;        // [NP] the t point's settled flags
+  const double x0 = x[i];
+  const Trial tr = trial_setup(x0, Q);
+  if (!tr.valid) {  // (never deferred: p = 0 settles at level 0)
+    if (lane == 0) lp[i] = node_logp(0.0, Q, K);
+    return;
+  }
+  const EngTables& T = et[node[i]];
+  const int flip = x0 > 0 ? 1 : 0;
+  const double a = Q.a, sv = Q.sv;
+  const double iwt = 1.0 / (T.tP[kTreeW] - T.tP[0]);
+  const double ia2 = 1.0 / (a * a);  // as l0_hints / refine_rounds
+  const L0Hints H = l0_hints(tr.x, T.tP[0], T.tP[kTreeW], a, K.err);
+  const double izf = T.iz[flip];
+  for (int e = lane; e < NE; e += 64) {
+    int k, gs, jh = -1;
+    if (e < NP * NG) {
+      k = e / NG;
+      gs = e - k * NG;
+      if (MODE == kAdaptT && (k & 3) == 0) jh = k >> 2;  // kAdaptT level 0: hinted
+    } else {
+      jh = e - NP * NG;
+      k = jh * (kTreeW / 4);
+      gs = kGridRoot;
+    }
+    double qh = -1.0;
+    bool known = false;
+    Decision kd{0, 0, 0};
+    if (jh >= 0) {
+      qh = H.qh(jh);
+      known = jh == 0 ? H.ok0 : (jh == 4 ? H.ok4 : H.shared);
+      kd = jh == 4 ? H.D4 : H.D0;
+    }
+    const TNode N = tnode_setup_r(tr.x - T.tP[k], tr.v, sv, a, ia2, K.err, qh, known, kd);
+    const int amb = N.amb ? (int)kFlagExact : 0;
+    if (MODE == kAdaptT) {
+      tv[k] = tnode_pdf_sv(N, tr.z, tr.v, sv, a) * iwt;
+      fp[k] = amb;
+    } else {
+      double y[5];
+      const bool ok = tnode_pdf_sv_grid5(N, T.G[flip][gs], tr.v, sv, a, y);  // literal values
+      if (jh < 0) {
+#pragma unroll
+        for (int j = 0; j < 5; ++j)
+          if (grid_owns(gs, j)) zv[k * NP + grid_point(gs, j)] = y[j] * izf;
+        if (gs == kGridRoot) fu[k] = amb | (ok ? 0 : kOvfBit);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 5; ++j) hv[jh * 5 + j] = y[j] * izf;
+        fh[jh] = amb | (ok ? 0 : kOvfBit);
+      }
+    }
+  }
+  wave_sync();
+  if (MODE == kAdaptTZ && lane < NP) {
+    // t point k's task completion (refine_rounds stage 0): the root test on
+    // its root grid (hinted at level 0), then -- if it refines or the grid
+    // overflowed -- the z walk over the unhinted grids
+    const int k = lane;
+    const bool l0 = (k & 3) == 0;
+    const double* r = l0 ? hv + (k >> 2) * 5 : nullptr;
+    const double r0 = l0 ? r[0] : zv[k * NP], r1 = l0 ? r[1] : zv[k * NP + 4],
+                 r2 = l0 ? r[2] : zv[k * NP + 8], r3 = l0 ? r[3] : zv[k * NP + 12],
+                 r4 = l0 ? r[4] : zv[k * NP + 16];
+    const int rf = l0 ? fh[k >> 2] : fu[k];
+    const ZGrid& gr = T.G[flip][kGridRoot];
+    const Simp sm = simp5p(gr.h6, gr.h12, r0, r1, r2, r3, r4);
+    int f = 0;
+    const bool ovf = (rf & kOvfBit) != 0;
+    const bool pend = simpson_refine(sm.S, sm.S2, K.simps_err, K.n_sz, f) || ovf;
+    if (ovf) f = 0;
+    int flags = (rf & kFlagExact) | f;
+    double val;
+    if (!pend) {
+      val = simp_value(sm) * iwt;
+    } else {
+      flags |= fu[k] & kFlagExact;  // the walk's own (unhinted) t node
+      const double(&zk)[kTreePoints] =
+          *reinterpret_cast<const double(*)[kTreePoints]>(zv + k * NP);
+      int f2 = 0, nref = 0;
+      unsigned need = 0u;
+      const double zi = tree17(zk, T.zP[flip], K.simps_err, K.n_sz, kTreeDepth, f2, need, nref);
+      if (need) f2 |= kFlagFallback;  // z tree deeper than the walk's levels
+      flags |= f2 & (kFlagExact | kFlagFallback);
+      val = zi * iwt;
+    }
+    tv[k] = val;
+    fp[k] = flags;
+  }
+  wave_sync();
+  if (lane == 0) {
+    const double(&tk)[kTreePoints] = *reinterpret_cast<const double(*)[kTreePoints]>(tv);
+    unsigned need = 0u, used = 0u;
+    int fl = 0, nref = 0;
+    double p = tree17(tk, T.tP, K.simps_err, K.n_st, kTreeDepth, fl, need, nref, &used);
+#pragma unroll 1
+    for (int k = 0; k < NP; ++k)
+      if ((used >> k) & 1u) fl |= fp[k];
+    if (need) fl |= kFlagFallback;  // t tree deeper than kTreeDepth
+    fl &= kFlagExact | kFlagFallback;
+    // tree_density's settlement
+    const bool structural = tr.x - T.tP[0] <= 0;
+    bool defer = fl != 0 || !(p > kExactBelow || structural);
+    if (defer && fl == 0 && tiny_absorbed(p, Q.p_outlier, K.w_outlier)) {
+      defer = false;
+      p = 0.0;
+    }
+    if (defer) {
+      long long n1 = 0;
+      p = (fl & kFlagExact) || fl == 0 ? exact_pdf(x0, Q, K, &n1, &errf)
+                                       : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+    }
+    lp[i] = node_logp(p, Q, K);
+  }
+  wave_sync();  // the next record reuses the wave's LDS
+}
+
 // The node path's completion of the chunks node_fast_kernel listed: one wave
 // per chunk, as the dataset engine (engine_kernel) runs a chunk, per node
 // segment of the chunk (nodes are contiguous and |rt|-ordered: a chunk holds
@@ -1898,7 +2062,7 @@ template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
-    unsigned long long* evals, int* status, int* prof) {
+    unsigned long long* evals, int* status, int* prof, const EngTables* et) {
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
@@ -1907,6 +2071,16 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
   const int w0 =
       __builtin_amdgcn_readfirstlane((int)blockIdx.x * kEngWaves + (int)(threadIdx.x >> 6));
   if (node_records_sparse(nrec, nc)) {  // a few deferred trials: one wave each
+    if constexpr (!COUNT && (MODE == kAdaptT || MODE == kAdaptTZ)) {
+      if (et) {  // the call's node tables exist: every tree point in two rounds
+        int errf = 0;
+        for (int k = w0; k < nrec; k += nwaves)
+          node_record_spec<MODE>(cl.F, cl.X, cl.fl, lane, x, node, K, lp, r_idx[k], r_par[k],
+                                 et, errf);  // F: 1088 doubles, fl: 64 ints
+        if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
+        return;
+      }
+    }
     node_records<MODE, COUNT, false>(cl, lane, w0, nwaves, x, K, lp, r_idx, r_par, nrec, evals,
                                      status);
     return;
@@ -2363,10 +2537,10 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     if (nt && nt->n_nodes > 0) {
       // the call's node tables, then the t-node split level 0; the chunk
       // engine / records below read the device copy of the rows
-      hipLaunchKernelGGL(node_grid_kernel, dim3((2 * nt->n_nodes + 255) / 256), dim3(256), 0, s,
-                         P, nt->n_nodes, nt->prow, nt->ngrid, MODE == kAdaptTZ ? 1 : 0);
+      hipLaunchKernelGGL(node_grid_kernel, dim3((8 * nt->n_nodes + 255) / 256), dim3(256), 0, s,
+                         P, nt->n_nodes, nt->prow, nt->etab, MODE == kAdaptTZ ? 1 : 0);
       hipLaunchKernelGGL((node_split_kernel<MODE>), dim3((n + 63) / 64), dim3(kNodeSplit * 64), 0,
-                         s, x, node, n, nt->prow, nt->ngrid, K, lp, d_idx, d_par, clist, n_defer);
+                         s, x, node, n, nt->prow, nt->etab, K, lp, d_idx, d_par, clist, n_defer);
       P = nt->prow;
       split = true;
     }
@@ -2382,7 +2556,8 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     const int64_t nw = (n + 63) / 64;
     const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
-                       n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof);
+                       n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof,
+                       split ? nt->etab : nullptr);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;
