@@ -285,34 +285,39 @@ class Dataset:
         return (out.value, terms) if trials else out.value
 
     def _node_table(self, params):
+        """The (n_nodes, 8) parameter table as a wfpt_params pointer, zero-copy
+        (wfpt_params is 8 doubles, the row layout of a C-contiguous float64
+        array); returns (pointer, the array that owns the memory)."""
         if self.n_nodes == 0:
             raise ValueError("dataset was created without node ids")
-        pm = np.ascontiguousarray(np.asarray(params, dtype=np.float64))
+        pm = np.ascontiguousarray(params, dtype=np.float64)
         if pm.shape != (self.n_nodes, 8):
             raise ValueError(f"params must have shape ({self.n_nodes}, 8)")
-        return (_lib.Params * self.n_nodes).from_buffer_copy(pm.tobytes())
+        return pm.ctypes.data_as(_lib._PP), pm
 
     def wiener_like_nodes_local(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
                                 simps_err=1e-3, w_outlier=0.1):
         """This shard's per-node partial sums and its encoded error count
         (n_nodes + 1 values): what wiener_like_nodes_allreduce sums over ranks."""
-        table = self._node_table(params)
-        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        table, keep = self._node_table(params)
+        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = np.empty(self.n_nodes + 1, dtype=np.float64)
         _lib.check(_lib.wfpt_wiener_like_nodes_local(self.ctx.handle, self.handle, table,
                                                      ctypes.byref(K), _lib.dptr(out)))
+        del keep
         return out
 
     def wiener_like_nodes_allreduce(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
                                     simps_err=1e-3, w_outlier=0.1):
         """Per-node sums over every rank's shard (hddm_amd.dist.init_comm):
         one all-reduce of n_nodes + 1 doubles per call."""
-        table = self._node_table(params)
-        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        table, keep = self._node_table(params)
+        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = np.empty(self.n_nodes, dtype=np.float64)
         _lib.check(_lib.wfpt_wiener_like_nodes_allreduce(self.ctx.handle, self.handle, table,
                                                          self.n_nodes, ctypes.byref(K),
                                                          _lib.dptr(out)))
+        del keep
         return out
 
     def wiener_like_nodes(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
@@ -321,13 +326,8 @@ class Dataset:
         Returns the per-node summed log-likelihoods (float64[n_nodes]);
         trials=True: (per-node sums, per-trial log terms in the order the
         trials were given to the Dataset)."""
-        if self.n_nodes == 0:
-            raise ValueError("dataset was created without node ids")
-        pm = np.ascontiguousarray(np.asarray(params, dtype=np.float64))
-        if pm.shape != (self.n_nodes, 8):
-            raise ValueError(f"params must have shape ({self.n_nodes}, 8)")
-        table = (_lib.Params * self.n_nodes).from_buffer_copy(pm.tobytes())
-        K = _lib.make_knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        table, keep = self._node_table(params)
+        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = np.empty(self.n_nodes, dtype=np.float64)
         if trials:
             terms = np.empty(self.n, dtype=np.float64)
@@ -337,4 +337,5 @@ class Dataset:
             return out, terms
         _lib.check(_lib.wfpt_wiener_like_nodes(self.ctx.handle, self.handle, table,
                                                ctypes.byref(K), _lib.dptr(out)))
+        del keep
         return out

@@ -26,6 +26,26 @@ def _free_port():
     return p
 
 
+def _master_store():
+    """A TCPStore master held by the test process on a port the OS assigned
+    and that stays bound (a probed-then-released port can be taken by another
+    socket before a rank binds it: EADDRINUSE); the ranks join it as clients.
+    Returns (store, port); keep the store alive until the ranks have joined."""
+    import torch.distributed as dist
+    store = dist.TCPStore("127.0.0.1", 0, is_master=True, wait_for_workers=False)
+    return store, store.port
+
+
+def _init_pg(rank, world, port):
+    """A rank joins the test process's store (_master_store) and forms the
+    gloo group through it."""
+    import datetime
+    import torch.distributed as dist
+    store = dist.TCPStore("127.0.0.1", port, is_master=False,
+                          timeout=datetime.timedelta(seconds=60))
+    dist.init_process_group("gloo", store=store, rank=rank, world_size=world)
+
+
 def _worker(rank, world, port, x, args, kn, inject, out_q):
     import sys
     sys.path.insert(0, ROOT)
@@ -34,9 +54,7 @@ def _worker(rank, world, port, x, args, kn, inject, out_q):
     import oracle
     from hddm_amd import _lib
     from hddm_amd import dist as hdist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init_pg(rank, world, port)
     lo, hi = hdist.shard_range(x.size, world, rank)
     lp = oracle.pdf_array(x[lo:hi], *args, kn[0], 1, *kn[1:])
     zeros = int(np.isneginf(lp).sum())
@@ -74,9 +92,7 @@ def _device_worker(rank, world, port, x, args, kn, seq, out_q):
     import torch.distributed as dist
     from hddm_amd import _lib, wfpt
     from hddm_amd import dist as hdist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init_pg(rank, world, port)
     lo, hi = hdist.shard_range(x.size, world, rank)
     ds = wfpt.Dataset(x[lo:hi])
     res = []
@@ -94,16 +110,16 @@ def _device_worker(rank, world, port, x, args, kn, seq, out_q):
 def _run(x, args, kn, inject, worker=None, extra=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    store, port = _master_store()
     if worker is None:
         worker, extra = _worker, inject
     procs = [ctx.Process(target=worker, args=(r, 2, port, x, args, kn, extra, q))
              for r in range(2)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = [q.get(timeout=100) for _ in procs]
     for p in procs:
-        p.join(timeout=60)
+        p.join(timeout=30)
         assert p.exitcode == 0
     assert sum(r[2] for r in res) == x.size
     return [r[1] for r in res]
@@ -397,9 +413,7 @@ def _node_worker(rank, world, port, x, node, params, kn, out_q):
     import torch.distributed as dist
     from hddm_amd import _lib, wfpt
     from hddm_amd import dist as hdist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _init_pg(rank, world, port)
     lo, hi = hdist.shard_range(x.size, world, rank)
     ds = wfpt.Dataset(x[lo:hi], node_id=node[lo:hi], n_nodes=params.shape[0])
     v = torch.tensor(ds.wiener_like_nodes_local(params, *kn), dtype=torch.float64)
@@ -435,14 +449,14 @@ def test_two_rank_gloo_node_sums(gpu, oracle_lib):
             want = gpu.Dataset(xx, node_id=node, n_nodes=m).wiener_like_nodes(pz, *kn)
         ctx = mp.get_context("spawn")
         q = ctx.Queue()
-        port = _free_port()
+        store, port = _master_store()
         procs = [ctx.Process(target=_node_worker, args=(r, 2, port, xx, node, pz, kn, q))
                  for r in range(2)]
         for p in procs:
             p.start()
-        res = [q.get(timeout=120) for _ in procs]
+        res = [q.get(timeout=100) for _ in procs]
         for p in procs:
-            p.join(timeout=60)
+            p.join(timeout=30)
             assert p.exitcode == 0
         for _, got, _ in res:
             fin = np.isfinite(want)
