@@ -139,11 +139,8 @@ struct wfpt_ctx {
   DevBuf<int> rflag;         // per slot: kFlagExact | kFlagFallback
   DevBuf<unsigned char> redo;  // per chunk: the lean pass left it to the engine (0 at rest)
   int* tree_any = nullptr;   // device: some chunk refined in-wave (finalize reports + clears)
-  DevBuf<double> fin;        // device: the H64 reduction's level-1 results (3 x groups)
-  int* fin_ticket = nullptr; // device: finalize_kernel's last-block ticket (0 at rest)
-  DevBuf<int> gcnt;          // device: the fused reduction's per-group counters (0 at rest)
-  int* fin_top = nullptr;    // device: the fused reduction's group ticket (0 at rest)
-  bool fuse = true;          // WFPT_FUSE=0: level-0-only passes keep a finalize launch
+  double* fin = nullptr;     // device: multi-block finalize scratch (3 x 64 doubles)
+  int* fin_ticket = nullptr; // device: its last-block ticket (0 at rest)
   int* prof = nullptr;       // device: 16 refinement work counters (PROF_EVALS)
   unsigned long long* phase = nullptr;  // device: engine phase cycles (diagnostic builds)
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
@@ -166,7 +163,13 @@ struct wfpt_ctx {
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
-  bool node_split = true;      // WFPT_NODE_SPLIT=0: the per-node level 0 one lane per trial
+  // WFPT_NODE_SPLIT=1: the per-node level 0 of the adaptive t families split
+  // over five lanes per trial (node_split_kernel; measured slower on config 4:
+  // the per-lane grid and hints are redone by every lane); WFPT_NODE_SPEC=0:
+  // sparse deferred trials through the breadth-first rounds instead of
+  // node_record_spec
+  bool node_split = false;
+  bool node_spec = true;
   bool fast_only = true;       // WFPT_FAST_ONLY=0: resident calls always enqueue the slow pass
   bool lean = true;            // WFPT_LEAN=0: resident calls never use the lean level-0 pass
   bool small = true;           // WFPT_SMALL=0: one-block calls keep the separate finalize
@@ -421,25 +424,9 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
     }
   }
   const wfpt::Split S = eng ? split_of(d) : wfpt::Split{};
-  // the H64 reduction's scratch: level-1 results of ceil(nb / 64) groups
-  const int64_t ng = (nb + 63) / 64;
-  HIP_TRY(c->fin.reserve(3 * (size_t)std::max<int64_t>(ng, 64)));
-  const int64_t fcap = (int64_t)(c->fin.cap / 3);
-  // a level-0-only pass of more than one block reduces its own chunk
-  // partials (the fused reduction): no finalize launch
-  const bool fuse = c->fuse && level0_only && !mirror && !c->count && n > 256;
-  wfpt::FuseArgs Fu{};
-  if (fuse) {
-    if (c->gcnt.cap < (size_t)ng) {
-      HIP_TRY(c->gcnt.reserve(ng));
-      HIP_TRY(hipMemsetAsync(c->gcnt.p, 0, c->gcnt.cap * sizeof(int), c->stream));
-    }
-    Fu = wfpt::FuseArgs{c->fin.p, fcap, c->gcnt.p, c->fin_top, c->status, out, ++c->seq,
-                        c->tree_any};
-  }
   wfpt::launch_trials(c->trial ? 3 : 0, adaptive ? part : wfpt::kPassAll, dx, n, P, K, c->part.p,
                       c->zero.p, c->count ? c->evals : nullptr, c->status, 0, W, c->stream,
-                      prof ? c->ev1 : nullptr, &S, c->trial, fuse ? &Fu : nullptr);
+                      prof ? c->ev1 : nullptr, &S, c->trial);
   if (!adaptive) {
     c->path |= WFPT_PATH_FIXED;
   } else {
@@ -452,11 +439,10 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
     if (part & wfpt::kPassDeferred) c->path |= WFPT_PATH_FOLD;
   }
   HIP_TRY(hipGetLastError());
-  if (fuse) return WFPT_OK;
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, adaptive ? 1 : 0,
                         c->status, out, ++c->seq, c->stream, eng ? S.next_n : nullptr,
-                        eng ? d->hcount + d->parity : nullptr, c->tree_any, mirror, c->fin.p,
-                        fcap, c->fin_ticket);
+                        eng ? d->hcount + d->parity : nullptr, c->tree_any, mirror, c->fin,
+                        c->fin_ticket);
   HIP_TRY(hipGetLastError());
   return WFPT_OK;
 }
@@ -663,11 +649,11 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* sm = std::getenv("WFPT_SYNC")) c->spin = std::strcmp(sm, "stream") != 0;
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* ns = std::getenv("WFPT_NODE_SPLIT")) c->node_split = std::strcmp(ns, "0") != 0;
+  if (const char* nq = std::getenv("WFPT_NODE_SPEC")) c->node_spec = std::strcmp(nq, "0") != 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
   if (const char* sm = std::getenv("WFPT_SMALL")) c->small = std::strcmp(sm, "0") != 0;
   if (const char* lt = std::getenv("WFPT_LEAN_TREE")) c->lean_tree_max = std::atof(lt);
-  if (const char* fu = std::getenv("WFPT_FUSE")) c->fuse = std::strcmp(fu, "0") != 0;
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipEventCreate(&c->ev0);
   if (e == hipSuccess) e = hipEventCreate(&c->ev1);
@@ -685,9 +671,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (e == hipSuccess) e = hipMemset(c->ncnt, 0, 4 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&c->tree_any, sizeof(int));
   if (e == hipSuccess) e = hipMemset(c->tree_any, 0, sizeof(int));
-  if (e == hipSuccess) e = c->fin.reserve(3 * 64);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->fin_top, sizeof(int));
-  if (e == hipSuccess) e = hipMemset(c->fin_top, 0, sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->fin, 3 * 64 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&c->ar, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMemset(c->ar, 0, 8 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&c->fin_ticket, sizeof(int));
@@ -739,9 +723,7 @@ void wfpt_close(wfpt_ctx* c) {
   if (c->ncnt) (void)hipFree(c->ncnt);
 
   if (c->tree_any) (void)hipFree(c->tree_any);
-  c->fin.release();
-  c->gcnt.release();
-  if (c->fin_top) (void)hipFree(c->fin_top);
+  if (c->fin) (void)hipFree(c->fin);
   if (c->fin_ticket) (void)hipFree(c->fin_ticket);
   if (c->ar) (void)hipFree(c->ar);
   c->redo.release();
@@ -1072,7 +1054,7 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
   // the split level 0 (adaptive t families, non-counting calls): the call's
   // node rows + root z grids in device memory
   const bool split = (mode == wfpt::kAdaptT || mode == wfpt::kAdaptTZ) && !c->count && c->node_split;
-  const wfpt::NodeTables nt{m};
+  const wfpt::NodeTables nt{m, split, !c->count && c->node_spec};
   c->path = split ? WFPT_PATH_NODE_SPLIT : 0;
   HIP_TRY(c->mnode.reserve((size_t)m + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
@@ -1080,7 +1062,7 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, mode, c->lp.p, c->nd_idx.p,
                      c->nd_par.p, c->ncnt, c->nd_chunks.p, c->count ? c->evals : nullptr,
-                     c->status, c->prof, c->stream, split ? &nt : nullptr);
+                     c->status, c->prof, c->stream, &nt);
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
   return WFPT_OK;
@@ -1267,10 +1249,8 @@ int run_multi(wfpt_ctx* c, const double* dx, int64_t n, const double* const arra
   }
   HIP_TRY(hipGetLastError());
   if (c->profile) HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  HIP_TRY(c->fin.reserve(3 * (size_t)std::max<int64_t>((nb + 63) / 64, 64)));
   wfpt::launch_finalize(c->part.p, c->zero.p, nb, 0, c->status, c->mres_dev, ++c->seq,
-                        c->stream, nullptr, nullptr, nullptr, nullptr, c->fin.p,
-                        (int64_t)(c->fin.cap / 3), c->fin_ticket);
+                        c->stream, nullptr, nullptr, nullptr, nullptr, c->fin, c->fin_ticket);
   HIP_TRY(hipGetLastError());
   if (int rc = wait_result(c, c->mres)) return rc;
   if (int rc = check_status_value(c->mres[2])) return rc;

@@ -82,26 +82,10 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K);
 // chunks (before the fold). fast_done (optional) is recorded right after the
 // level-0 / trial kernel.
 constexpr int kPassFast = 1, kPassDeferred = 2, kPassAll = 3, kPassLean = 4, kPassRedo = 8;
-// The fused reduction of a level-0-only pass (lean_kernel / fast_kernel<kDirect>
-// with FUSE, wfpt_kernels.hip: fuse_tail): the launch also does the finalize
-// (the H64 reduction, fin_write into `out`), so no finalize_kernel follows.
-struct FuseArgs {
-  double* fin;     // [3 cap] level-1 results
-  int64_t cap;     // >= number of H64 groups, ceil(chunks / 64)
-  int* gcnt;       // [groups] blocks arrived per group (0 at rest)
-  int* top;        // groups finished (0 at rest)
-  int* status;
-  double* out;     // the call's result slot
-  unsigned long long seq;
-  int* tree_any;
-};
-// fuse (optional, level-0-only passes of OUT_SUM / OUT_BOTH without
-// evaluation counting): the fused reduction instead of a finalize launch.
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done = nullptr,
-                   const Split* split = nullptr, double* trial = nullptr,
-                   const FuseArgs* fuse = nullptr);
+                   const Split* split = nullptr, double* trial = nullptr);
 // out[0..3] = {sum of nb partials, #zero trials, encoded error flags,
 // kResDeferred (defer_bits: some chunk's zero word carries kZeroDefer) |
 // kResTree (*tree_any; then *tree_any = 0)}, out[6] = *tree_any (chunks that
@@ -110,12 +94,11 @@ void launch_trials(int out_kind, int part, const double* x, int64_t n, const Par
 // they are visible; resets *status to 0. mirror (optional, device memory):
 // out[0..3] and out[5] written there too.
 constexpr int kResDeferred = 1, kResTree = 2;
-// fin (device, 3 fin_cap doubles, fin_cap >= ceil(nb / 64)) + ticket (device
-// int, 0 at rest): the H64 reduction's level-1 results and last-block ticket.
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
-                     const int* split_rd, int* split_rs, int* tree_any, double* mirror,
-                     double* fin, int64_t fin_cap, int* ticket);
+                     const int* split_rd = nullptr, int* split_rs = nullptr,
+                     int* tree_any = nullptr, double* mirror = nullptr,
+                     double* fin = nullptr, int* ticket = nullptr);
 // One-block call (n <= 256, direct or adaptive family, level-0 pass + the
 // finalize in one launch: the same result bits and completion word as
 // launch_trials(kPassFast [| kPassLean]) + launch_finalize). kSmallNone: not
@@ -126,6 +109,8 @@ constexpr int kSmallNone = 0, kSmallOne = 1, kSmallSplit = 2;
 int launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, double* part,
                  int* zeros, int* status, const Work& W, double* out, unsigned long long seq,
                  int* tree_any, hipStream_t s, double* trial = nullptr);
+// fin (device, 3 * 64 doubles) + ticket (device int, 0 at rest): scratch of the
+// multi-block finalize for large nb (nullptr: one block)
 // res[0..3], res[5] (device) -> out[0..3], out[5] (mapped host), then
 // out[4] = seq.
 void launch_publish(const double* res, double* out, unsigned long long seq, hipStream_t s);
@@ -144,8 +129,11 @@ void launch_poison(double* res, hipStream_t s);
 // nt (optional): the call's node tables (device); with them the adaptive t
 // families (kAdaptT, kAdaptTZ) of a non-counting call run node_grid_kernel +
 // node_split_kernel (five lanes per trial) instead of node_fast_kernel.
-struct NodeTables {  // the split path's switch (launch_nodes)
+// split: the adaptive t families take node_split_kernel; spec: the sparse
+// deferred trials take node_record_spec (non-counting calls)
+struct NodeTables {
   int32_t n_nodes;
+  bool split, spec;
 };
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,

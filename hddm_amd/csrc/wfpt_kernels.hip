@@ -158,227 +158,11 @@ __device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defe
   return b != 0ull;
 }
 
-// ---------------------------------------------------------------------------
-// The likelihood's reduction (H64): one fixed order for a given number nb of
-// partials, whichever kernels produce the sum (finalize_kernel, the fused
-// lean pass, the one-block kernels), so a likelihood is bitwise reproducible
-// across call sequences:
-//   level 1: group g = partials [64 g, 64 g + 64) (0.0 beyond nb), each
-//            partial on lane (its index - 64 g), wave_sum;
-//   level 2: the ng = ceil(nb / 64) group sums over 256 threads: thread k
-//            adds groups k, k + 256, ... to 0.0 in that order, wave_sum per
-//            wave, then the 4 wave sums are added to 0.0 in wave order.
-// Zero counts (the low 16 bits of each zero word) are summed as integers and
-// the kZeroDefer bits OR-ed (defer_bits: per-chunk partials of the adaptive /
-// direct families).
-// Cross-block hand-offs use write-through (sc1) stores drained by
-// s_waitcnt vmcnt(0) before an agent-scope ticket add, and sc1 loads after
-// it (MI355X_MICROARCH.md, inter-workgroup visibility: no fences).
-__device__ inline void st_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void st_sc1(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline int ld_sc1(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ inline int ticket_add(int* t) {
-  return __hip_atomic_fetch_add(t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-struct Red {
-  double s;
-  long long z;
-  int d;
-};
-// Level 1 of group g (one wave; the result in every lane). SC1: the partials
-// were written by other blocks of this launch.
-template <bool SC1>
-__device__ inline Red h64_group(const double* part, const int* zeros, int64_t nb, int64_t g,
-                                int lane, int defer_bits) {
-  const int64_t c = g * 64 + lane;
-  double v = 0.0;
-  int w = 0;
-  if (c < nb) {
-    v = SC1 ? ld_sc1(part + c) : part[c];
-    w = SC1 ? ld_sc1(zeros + c) : zeros[c];
-  }
-  Red r;
-  r.s = wave_sum(v);
-  r.z = wave_sum_ll(w & (kZeroDefer - 1));
-  r.d = (defer_bits && __ballot((w & kZeroDefer) != 0) != 0ull) ? 1 : 0;
-  return r;
-}
-// Level 2 over the group results in global memory (s1[g], z1[g], d1[g]: sc1),
-// by the block's first 256 threads (every thread of the block calls it: it
-// has a barrier); thread 0 returns the total.
-__device__ inline Red h64_top(const double* s1, const double* z1, const double* d1, int64_t ng) {
-  __shared__ double ws[4];
-  __shared__ long long wz[4];
-  __shared__ int wd[4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  double s = 0.0;
-  long long z = 0;
-  int d = 0;
-  if (tid < 256) {
-#pragma unroll 1
-    for (int64_t g0 = tid; g0 < ng; g0 += 4 * 256) {
-      double v[4], zv[4], dv[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t g = g0 + q * 256;
-        v[q] = g < ng ? ld_sc1(s1 + g) : 0.0;
-        zv[q] = g < ng ? ld_sc1(z1 + g) : 0.0;
-        dv[q] = g < ng ? ld_sc1(d1 + g) : 0.0;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (g0 + q * 256 < ng) s += v[q];
-        z += (long long)zv[q];
-        d |= dv[q] != 0.0;
-      }
-    }
-    s = wave_sum(s);
-    z = wave_sum_ll(z);
-    const bool anyd = __ballot(d != 0) != 0ull;
-    if (lane == 0) {
-      ws[w] = s;
-      wz[w] = z;
-      wd[w] = anyd;
-    }
-  }
-  __syncthreads();
-  Red r{0.0, 0, 0};
-  if (tid == 0) {
-    for (int k = 0; k < 4; ++k) {
-      r.s += ws[k];
-      r.z += wz[k];
-      r.d |= wd[k];
-    }
-  }
-  return r;
-}
-// Level 2 of a single group (nb <= 64: the one-block kernels), by one wave:
-// the same operations as h64_top with one nonzero thread; lane 0 returns.
-__device__ inline double h64_single(double s1, int lane) {
-  double s = lane == 0 ? 0.0 + s1 : 0.0;
-  s = wave_sum(s);
-  double t = 0.0;
-  t += s;
-  t += 0.0;
-  t += 0.0;
-  t += 0.0;
-  return t;
-}
-
-// The result slot of a call (finalize's last step, one thread): {sum, zero
-// count, encoded errors, flags, -, heavy chunks, #tree} and then the 64-bit
-// completion word out[4] once they are visible (`out` may be mapped pinned
-// host memory); resets the device status word. out[3] = kResDeferred if some
-// chunk's word carries kZeroDefer | kResTree (some chunk refined in-wave).
-// The status and tree words are read and reset with device-scope atomics
-// (the fused lean pass's last block reads them in the launch that set them).
-__device__ inline void fin_write(double t, long long zz, int dd, int* status, double* out,
-                                 unsigned long long seq, const int* split_rd, int* split_rs,
-                                 int* tree_any, double* mirror) {
-  const int st = atomicExch(status, 0);
-  out[0] = t;
-  out[1] = (double)zz;
-  out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
-  int res3 = dd ? kResDeferred : 0;
-  double ntree = 0.0;
-  if (tree_any) {
-    const int ta = atomicExch(tree_any, 0);
-    if (ta) res3 |= kResTree;
-    ntree = (double)ta;
-  }
-  out[6] = ntree;
-  out[3] = (double)res3;
-  // heavy chunks recorded for the next call (Split)
-  out[5] = split_rd ? (double)*split_rd : 0.0;
-  if (split_rs) *split_rs = 0;
-  if (mirror) {  // device copy of the result (the RCCL exchange reads it)
-    mirror[0] = out[0];
-    mirror[1] = out[1];
-    mirror[2] = out[2];
-    mirror[3] = out[3];
-    mirror[5] = out[5];
-    mirror[6] = out[6];
-  }
-  __threadfence_system();
-  // completion word, written after the results are visible: the host may
-  // poll it instead of waiting on the stream
-  reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
-  __threadfence_system();
-}
-
-// The fused pass's reduction (FUSE: the predicted level-0-only resident call
-// of more than one block): each wave's chunk partial and zero word are
-// stored write-through (sc1) and drained; then per block one agent-scope
-// ticket add on its group's counter (16 blocks = the 64 chunks of one H64
-// group); the group's last block runs level 1 (wave 0) and adds to the call's
-// ticket; the call's last group runs level 2 and fin_write. Counters are 0 at
-// rest (each last arriver resets its own). No launch of finalize_kernel, the
-// same bits.
-template <bool FUSE>
-__device__ inline void fuse_tail(const TrialArgs& A, const FuseArgs& Fu) {
-  if constexpr (FUSE) {
-    __shared__ int role;
-    const int lane = threadIdx.x & 63;
-    const int64_t nb = (A.n + 63) / 64;
-    const int64_t ng = (nb + 63) / 64;
-    const int64_t g = (int64_t)blockIdx.x / 16;
-    drain_stores();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const int64_t b_lo = g * 16;
-      const int64_t b_hi = b_lo + 16 < (int64_t)gridDim.x ? b_lo + 16 : (int64_t)gridDim.x;
-      role = ticket_add(Fu.gcnt + g) == (int)(b_hi - b_lo) - 1;
-      if (role) Fu.gcnt[g] = 0;
-    }
-    __syncthreads();
-    if (!role) return;
-    if (threadIdx.x < 64) {
-      const Red r = h64_group<true>(A.out, A.zeros, nb, g, lane, 1);
-      if (lane == 0) {
-        st_sc1(Fu.fin + g, r.s);
-        st_sc1(Fu.fin + Fu.cap + g, (double)r.z);
-        st_sc1(Fu.fin + 2 * Fu.cap + g, (double)r.d);
-        drain_stores();
-        role = ticket_add(Fu.top) == (int)ng - 1;
-        if (role) *Fu.top = 0;
-      }
-    }
-    __syncthreads();
-    if (!role) return;
-    const Red t = h64_top(Fu.fin, Fu.fin + Fu.cap, Fu.fin + 2 * Fu.cap, ng);
-    if (threadIdx.x == 0)
-      fin_write(t.s, t.z, t.d, Fu.status, Fu.out, Fu.seq, nullptr, nullptr, Fu.tree_any, nullptr);
-  }
-}
-// A chunk's partial and zero word (lane 0): plain stores, or write-through
-// ones when the same launch reduces them (FUSE).
-template <bool FUSE>
-__device__ inline void put_chunk(const TrialArgs& A, int64_t c, double part, int zw) {
-  if (FUSE) {
-    st_sc1(A.out + c, part);
-    st_sc1(A.zeros + c, zw);
-  } else {
-    A.out[c] = part;
-    A.zeros[c] = zw;
-  }
-}
-
 // Direct family (sz = st = 0): one pdf_sv per trial, one chunk of 64 trials
 // per wave.
-template <int MODE, bool COUNT, int OUT, bool FUSE = false>
+template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void fast_kernel(TrialArgs A, Work W, FuseArgs Fu) {
+void fast_kernel(TrialArgs A, Work W) {
   const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
@@ -390,19 +174,20 @@ void fast_kernel(TrialArgs A, Work W, FuseArgs Fu) {
   double lp = 0.0;
   int zero = 0;
   if (i < A.n && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
-  if (c * 64 < A.n) {  // a wave past the last chunk has no outputs (wave-uniform)
-    const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
-    if (sum_out(OUT)) {
-      lp = wave_sum(lp);
-      const int zs = __popcll(__ballot(zero != 0));
-      if (lane == 0) put_chunk<FUSE>(A, c, lp, zs | (anyd ? kZeroDefer : 0));
-    }
-    if (COUNT) {
-      const long long nf = wave_sum_ll(oc == kFinal ? ne : 0);
-      if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
+  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
+  const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
+  if (sum_out(OUT)) {
+    lp = wave_sum(lp);
+    const int zs = __popcll(__ballot(zero != 0));
+    if (lane == 0) {
+      A.out[c] = lp;
+      A.zeros[c] = zs | (anyd ? kZeroDefer : 0);
     }
   }
-  fuse_tail<FUSE>(A, Fu);
+  if (COUNT) {
+    const long long nf = wave_sum_ll(oc == kFinal ? ne : 0);
+    if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -814,7 +599,7 @@ __device__ inline void tree_density(const TrialArgs& A, const ChunkLds<TW>& cl, 
 
 // Chunk outputs of the owner lanes (one wave): per-trial emit, deferred
 // slots, the chunk partial and the evaluation count.
-template <bool COUNT, int OUT, bool FUSE = false>
+template <bool COUNT, int OUT>
 __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, int lane, double p,
                                  bool defer, int rf, long long ne) {
   const int64_t i = c * 64 + lane;
@@ -825,7 +610,10 @@ __device__ inline void chunk_out(const TrialArgs& A, const Work& W, int64_t c, i
   if (sum_out(OUT)) {
     lp = wave_sum(lp);
     const int zs = __popcll(__ballot(zero != 0));
-    if (lane == 0) put_chunk<FUSE>(A, c, lp, zs | (anyd ? kZeroDefer : 0));
+    if (lane == 0) {
+      A.out[c] = lp;
+      A.zeros[c] = zs | (anyd ? kZeroDefer : 0);
+    }
   }
   if (COUNT) {
     const long long nf = wave_sum_ll((i < A.n && !defer) ? ne : 0ll);
@@ -1074,10 +862,18 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 #define WFPT_SIN_TABLE 1
 #endif
 
-// lean_kernel's chunk (one wave).
-template <int MODE, bool COUNT, int OUT, bool FUSE>
-__device__ inline void lean_chunk(const TrialArgs& A, const Work& W, const RootGrids& R,
-                                  int64_t i, int64_t c, int lane) {
+template <int MODE, bool COUNT, int OUT>
+__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+void lean_kernel(TrialArgs A, Work W, RootGrids R) {
+#if WFPT_LEAN_REVERSE
+  // blocks dispatched last take the first chunks (timing experiment)
+  const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kFastBlock + threadIdx.x;
+#else
+  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
+#endif
+  const int lane = threadIdx.x & 63;
+  const int64_t c = i >> 6;
+  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
   const bool own = i < A.n;
   const double x0 = own ? A.x[i] : 0.0;
   double p = 0.0, f0[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -1106,29 +902,11 @@ __device__ inline void lean_chunk(const TrialArgs& A, const Work& W, const RootG
     if (lane == 0) {
       W.redo[c] = 1;
       // finalize reports the call as deferred: the host runs the redo pass
-      if (sum_out(OUT)) {
-        if (FUSE) st_sc1(A.zeros + c, kZeroDefer);
-        else A.zeros[c] = kZeroDefer;
-      }
+      if (sum_out(OUT)) A.zeros[c] = kZeroDefer;
     }
     return;
   }
-  chunk_out<COUNT, OUT, FUSE>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
-}
-
-template <int MODE, bool COUNT, int OUT, bool FUSE = false>
-__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
-void lean_kernel(TrialArgs A, Work W, RootGrids R, FuseArgs Fu) {
-#if WFPT_LEAN_REVERSE
-  // blocks dispatched last take the first chunks (timing experiment)
-  const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kFastBlock + threadIdx.x;
-#else
-  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
-#endif
-  const int lane = threadIdx.x & 63;
-  const int64_t c = i >> 6;
-  if (c * 64 < A.n) lean_chunk<MODE, COUNT, OUT, FUSE>(A, W, R, i, c, lane);  // wave-uniform
-  fuse_tail<FUSE>(A, Fu);
+  chunk_out<COUNT, OUT>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
 }
 
 // A node's trial term: mixture with the node's p_outlier, -inf for a zero
@@ -1316,64 +1094,155 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
   }
 }
 
-// The H64 sum of nb partials in one launch of G blocks of 1024 threads: wave
-// w of block b takes groups b 16 + w, + 16 G, ... (level 1, four loads in
-// flight per lane), writes their results to fin (sc1: s1 at fin[g], z1 at
-// fin[cap + g], d1 at fin[2 cap + g]); the last block to finish (agent-scope
-// ticket, 0 at rest) runs level 2 and fin_write. cap >= ceil(nb / 64).
+// out[0] = sum of nb partials, out[1] = number of zero trials, out[2] = error
+// flags encoded as counts that survive a sum over ranks (depth + 2^20 budget),
+// out[3] = kResDeferred if some chunk's word carries kZeroDefer (defer_bits:
+// per-chunk partials of the adaptive / direct families) | kResTree, then the
+// 64-bit completion word out[4] once they are visible. `out` may be mapped
+// pinned host memory. Resets the device status word. Fixed summation order
+// for a given nb: thread k owns partials k + 1024 j, loaded kFinLoads at a
+// time (all in flight together) and summed in j order; then a fixed tree.
+// The result slot of a call (finalize's last step, one thread): {sum, zero
+// count, encoded errors, flags, -, heavy chunks, #tree} and then the
+// completion word; resets the device status word.
+__device__ inline void fin_write(double t, long long zz, int dd, int* status, double* out,
+                                 unsigned long long seq, const int* split_rd, int* split_rs,
+                                 int* tree_any, double* mirror) {
+  const int st = *status;
+  *status = 0;
+  out[0] = t;
+  out[1] = (double)zz;
+  out[2] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+  int res3 = dd ? kResDeferred : 0;
+  double ntree = 0.0;
+  if (tree_any) {
+    if (*tree_any) res3 |= kResTree;
+    ntree = (double)*tree_any;
+    *tree_any = 0;
+  }
+  out[6] = ntree;
+  out[3] = (double)res3;
+  // heavy chunks recorded for the next call (Split)
+  out[5] = split_rd ? (double)*split_rd : 0.0;
+  if (split_rs) *split_rs = 0;
+  if (mirror) {  // device copy of the result (the RCCL exchange reads it)
+    mirror[0] = out[0];
+    mirror[1] = out[1];
+    mirror[2] = out[2];
+    mirror[3] = out[3];
+    mirror[5] = out[5];
+    mirror[6] = out[6];
+  }
+  __threadfence_system();
+  // completion word, written after the results are visible: the host may
+  // poll it instead of waiting on the stream
+  reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
+  __threadfence_system();
+}
+
+// Large nb (C2's 10M trials: 156k partials): one block is bound by a single
+// CU's load bandwidth (29 us), so gridDim.x = G > 1 blocks each reduce a
+// contiguous range the same way into fin[g] (sum), fin[kFinMaxBlocks + g]
+// (zero count), fin[2 kFinMaxBlocks + g] (defer bits), and the last block to
+// finish (agent-scope ticket) adds the G block results in g order. Fixed
+// order for a given (nb, G); G = 1 is the single-block order.
+constexpr int kFinLoads = 16;
 constexpr int kFinMaxBlocks = 64;
-constexpr int64_t kFinGroupsPerBlock = 64;  // level-1 groups per block when sizing G
+constexpr int64_t kFinPerBlock = 8192;  // partials per block when split
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
                                                         int64_t nb, int defer_bits,
                                                         int* status, double* out,
                                                         unsigned long long seq,
                                                         const int* split_rd, int* split_rs,
                                                         int* tree_any, double* mirror,
-                                                        double* fin, int64_t cap, int* ticket) {
+                                                        double* fin, int* ticket) {
+  __shared__ double ss[16];
+  __shared__ long long sz[16];
+  __shared__ int sd[16];
   __shared__ int last;
-  const int lane = threadIdx.x & 63;
-  const int64_t ng = (nb + 63) / 64;
-  const int64_t nw = (int64_t)gridDim.x * 16;
-  const int64_t w0 = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 6);
-#pragma unroll 1
-  for (int64_t g0 = w0; g0 < ng; g0 += 4 * nw) {
-    Red r[4];
+  const int G = gridDim.x;
+  int64_t lo = 0, hi = nb;
+  if (G > 1) {
+    const int64_t L = (nb + G - 1) / G;
+    lo = (int64_t)blockIdx.x * L;
+    hi = lo + L < nb ? lo + L : nb;
+  }
+  double s = 0.0;
+  long long z = 0;
+  int def = 0;
+  for (int64_t b0 = lo + threadIdx.x; b0 < hi; b0 += kFinLoads * 1024) {
+    double v[kFinLoads];
+    int w[kFinLoads];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r[q] = h64_group<false>(part, zeros, nb, g0 + q * nw, lane, defer_bits);
-    if (lane == 0) {
+    for (int j = 0; j < kFinLoads; ++j) {
+      const int64_t b = b0 + (int64_t)j * 1024;
+      v[j] = b < hi ? part[b] : 0.0;
+      w[j] = b < hi ? zeros[b] : 0;
+    }
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int64_t g = g0 + q * nw;
-        if (g < ng) {
-          st_sc1(fin + g, r[q].s);
-          st_sc1(fin + cap + g, (double)r[q].z);
-          st_sc1(fin + 2 * cap + g, (double)r[q].d);
-        }
-      }
+    for (int j = 0; j < kFinLoads; ++j) {
+      s += v[j];
+      z += w[j] & (kZeroDefer - 1);
+      def |= w[j];
     }
   }
-  drain_stores();
+  def = defer_bits ? (def & kZeroDefer) : 0;
+  s = wave_sum(s);
+  z = wave_sum_ll(z);
+  const bool anyd = __ballot(def != 0) != 0ull;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+    ss[w] = s;
+    sz[w] = z;
+    sd[w] = anyd;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    last = 1;
-    if (gridDim.x > 1) {
-      last = ticket_add(ticket) == (int)gridDim.x - 1;
-      if (last) *ticket = 0;  // ready for the next call (stream order)
+    double t = 0.0;
+    long long zz = 0;
+    int dd = 0;
+    for (int k = 0; k < 16; ++k) {
+      t += ss[k];
+      zz += sz[k];
+      dd |= sd[k];
     }
+    if (G > 1) {
+      fin[blockIdx.x] = t;
+      fin[kFinMaxBlocks + blockIdx.x] = (double)zz;
+      fin[2 * kFinMaxBlocks + blockIdx.x] = (double)dd;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      const int prev =
+          __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == G - 1;
+    } else {
+      last = 1;
+    }
+    if (G > 1 && last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      t = 0.0;
+      zz = 0;
+      dd = 0;
+      for (int g = 0; g < G; ++g) {
+        t += __hip_atomic_load(&fin[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        zz += (long long)__hip_atomic_load(&fin[kFinMaxBlocks + g], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+        dd |= (int)__hip_atomic_load(&fin[2 * kFinMaxBlocks + g], __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+      }
+      *ticket = 0;  // ready for the next call (stream order)
+    }
+    if (!last) return;
+    fin_write(t, zz, dd, status, out, seq, split_rd, split_rs, tree_any, mirror);
   }
-  __syncthreads();
-  if (!last) return;
-  const Red t = h64_top(fin, fin + cap, fin + 2 * cap, ng);
-  if (threadIdx.x == 0)
-    fin_write(t.s, t.z, t.d, status, out, seq, split_rd, split_rs, tree_any, mirror);
 }
 
 // One-block calls (n <= kFastBlock trials: an HDDM node's 250, the drop-in's
 // per-node call): the level-0 pass of the direct family (fast_kernel's
 // operations) or of the adaptive families (lean_kernel's), then the finalize
-// of the block's <= 4 chunk partials in the same launch, with the H64
-// reduction's exact operations on them (one group: h64_single), so the result
-// and the completion word are bit for bit those of the two-launch sequence. The
+// of the block's <= 4 chunk partials in the same launch, with finalize_kernel's
+// exact operations on them (thread k holds partial k, one wave sum, then the
+// 16 wave sums added in order, the 15 empty ones as +0.0), so the result and
+// the completion word are bit for bit those of the two-launch sequence. The
 // chunk partials and zero words are written as usual (a deferred pass after a
 // misprediction reads them).
 struct FinArgs {
@@ -1449,16 +1318,31 @@ __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, 
   }
   __syncthreads();
   if (wv != 0) return;
-  // the H64 reduction of the block's <= 4 chunk partials (one group)
-  const int nbk = (int)((A.n + 63) / 64);
-  const double pv = lane < nbk ? fp[lane] : 0.0;
-  const int pw = lane < nbk ? fz[lane] : 0;
-  const double s1 = wave_sum(pv);
-  const long long zs = wave_sum_ll(pw & (kZeroDefer - 1));
-  const bool anyd = F.defer_bits && __ballot((pw & kZeroDefer) != 0) != 0ull;
-  const double tot = h64_single(s1, lane);
-  if (lane == 0)
-    fin_write(tot, zs, anyd, F.status, F.out, F.seq, nullptr, nullptr, F.tree_any, nullptr);
+  const int nb = (int)((A.n + 63) / 64);
+  double s = 0.0;
+  long long z = 0;
+  int def = 0;
+  if (lane < nb) {
+    s += fp[lane];
+    z += fz[lane] & (kZeroDefer - 1);
+    def |= fz[lane];
+  }
+  def = F.defer_bits ? (def & kZeroDefer) : 0;
+  s = wave_sum(s);
+  z = wave_sum_ll(z);
+  const bool anyd = __ballot(def != 0) != 0ull;
+  if (lane == 0) {
+    double t = 0.0;
+    long long zz = 0;
+    int dd = 0;
+    const double ss[2] = {s, 0.0};
+    for (int k = 0; k < 16; ++k) {
+      t += ss[k == 0 ? 0 : 1];
+      zz += k == 0 ? z : 0ll;
+      dd |= k == 0 ? (int)anyd : 0;
+    }
+    fin_write(t, zz, dd, F.status, F.out, F.seq, nullptr, nullptr, F.tree_any, nullptr);
+  }
 }
 
 // One-block calls of the full DDM (kAdaptTZ: 25 pdf_sv evaluations per
@@ -1594,16 +1478,31 @@ __global__ __launch_bounds__(kSplitBlock) void small_split_kernel(TrialArgs A, W
   }
   __syncthreads();
   if (wv != 0) return;
-  // the H64 reduction of the block's <= 4 chunk partials (one group)
-  const int nbk = (int)((A.n + 63) / 64);
-  const double pv = lane < nbk ? fp[lane] : 0.0;
-  const int pw = lane < nbk ? fz[lane] : 0;
-  const double s1 = wave_sum(pv);
-  const long long zs = wave_sum_ll(pw & (kZeroDefer - 1));
-  const bool anyd = F.defer_bits && __ballot((pw & kZeroDefer) != 0) != 0ull;
-  const double tot = h64_single(s1, lane);
-  if (lane == 0)
-    fin_write(tot, zs, anyd, F.status, F.out, F.seq, nullptr, nullptr, F.tree_any, nullptr);
+  const int nb = (int)((A.n + 63) / 64);
+  double s = 0.0;
+  long long z = 0;
+  int def = 0;
+  if (lane < nb) {
+    s += fp[lane];
+    z += fz[lane] & (kZeroDefer - 1);
+    def |= fz[lane];
+  }
+  def = F.defer_bits ? (def & kZeroDefer) : 0;
+  s = wave_sum(s);
+  z = wave_sum_ll(z);
+  const bool anyd = __ballot(def != 0) != 0ull;
+  if (lane == 0) {
+    double tt = 0.0;
+    long long zz = 0;
+    int dd = 0;
+    const double ss[2] = {s, 0.0};
+    for (int q = 0; q < 16; ++q) {
+      tt += ss[q == 0 ? 0 : 1];
+      zz += q == 0 ? z : 0ll;
+      dd |= q == 0 ? (int)anyd : 0;
+    }
+    fin_write(tt, zz, dd, F.status, F.out, F.seq, nullptr, nullptr, F.tree_any, nullptr);
+  }
 }
 
 // Copies a device result {sum, zeros, errors} (after the RCCL all-reduce) to
@@ -1700,9 +1599,11 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
     const bool anyz = __ballot(zero != 0) != 0ull;
     if (lane == 0) out[j] = anyz ? -INFINITY : s;
   }
-  drain_stores();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) last = ticket_add(ticket) == (int)gridDim.x - 1;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.x - 1;
   __syncthreads();
   if (!last || threadIdx.x != 0) return;
   *ticket = 0;
@@ -2422,32 +2323,15 @@ static TrialArgs trial_args(const double* x, int64_t n, const Params& P, const K
 
 template <int MODE, bool COUNT, int OUT>
 static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
-                     bool lean, hipStream_t s, hipEvent_t fast_done, const FuseArgs* fu) {
-  const FuseArgs F0{};
+                     bool lean, hipStream_t s, hipEvent_t fast_done) {
   if constexpr (MODE == kDirect) {
-    if constexpr (!COUNT && sum_out(OUT)) {
-      if (fu) {
-        hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT, true>), dim3(fast_blocks(A.n)),
-                           dim3(kFastBlock), 0, s, A, W, *fu);
-        if (fast_done) (void)hipEventRecord(fast_done, s);
-        return;
-      }
-    }
     hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
-                       0, s, A, W, F0);
+                       0, s, A, W);
   } else if (lean) {
     RootGrids R;
     root_grids(A.P, R);
-    if constexpr (!COUNT && sum_out(OUT)) {
-      if (fu) {
-        hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT, true>), dim3(fast_blocks(A.n)),
-                           dim3(kFastBlock), 0, s, A, W, R, *fu);
-        if (fast_done) (void)hipEventRecord(fast_done, s);
-        return;
-      }
-    }
     hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
-                       0, s, A, W, R, F0);
+                       0, s, A, W, R);
   } else {
     const int64_t units = (int64_t)S.n * kSplit + (A.n + 63) / 64;
     hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>),
@@ -2473,7 +2357,7 @@ static void run_deferred(const TrialArgs& A, const Work& W, const EngTables& T, 
 
 template <bool COUNT, int OUT>
 static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, const Split& S,
-                        hipStream_t s, hipEvent_t fast_done, const FuseArgs* fu) {
+                        hipStream_t s, hipEvent_t fast_done) {
   // the engine's tables (the lean pass alone needs only its root grids)
   EngTables T;
   const bool engine = ((part & kPassFast) && !(part & kPassLean)) || (part & kPassRedo);
@@ -2486,7 +2370,7 @@ static void launch_mode(int mode, int part, const TrialArgs& A, const Work& W, c
 #define FAST_AND_DEFERRED(M_)                                                       \
   do {                                                                              \
     if (part & kPassFast)                                                           \
-      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, s, fast_done, fu);    \
+      run_fast<M_, COUNT, OUT>(A, F, T, S, (part & kPassLean) != 0, s, fast_done);        \
     if (part & kPassDeferred)                                                       \
       run_deferred<M_, COUNT, OUT>(A, F, T, (part & kPassRedo) != 0, s);            \
   } while (0)
@@ -2523,26 +2407,26 @@ int64_t partials_for(int64_t n, const Params& P, const Knobs& K) {
 void launch_trials(int out_kind, int part, const double* x, int64_t n, const Params& P,
                    const Knobs& K, double* out, int* zeros, unsigned long long* evals, int* status,
                    int logp, const Work& W, hipStream_t s, hipEvent_t fast_done,
-                   const Split* split, double* trial, const FuseArgs* fuse) {
+                   const Split* split, double* trial) {
   if (n <= 0) return;
   Split S{};
   if (split) S = *split;
   const TrialArgs A = trial_args(x, n, P, K, out, zeros, evals, status, logp, trial);
   const int mode = select_mode(P.sz, P.st, K.use_adaptive);
   if (out_kind == OUT_BOTH) {  // the per-trial check (no evaluation counting)
-    launch_mode<false, OUT_BOTH>(mode, part, A, W, S, s, fast_done, fuse);
+    launch_mode<false, OUT_BOTH>(mode, part, A, W, S, s, fast_done);
     return;
   }
   if (evals) {
-    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, S, s, fast_done, nullptr);
+    if (out_kind == OUT_SUM) launch_mode<true, OUT_SUM>(mode, part, A, W, S, s, fast_done);
     else if (out_kind == OUT_ARRAY)
-      launch_mode<true, OUT_ARRAY>(mode, part, A, W, S, s, fast_done, nullptr);
-    else launch_mode<true, OUT_LOGP>(mode, part, A, W, S, s, fast_done, nullptr);
+      launch_mode<true, OUT_ARRAY>(mode, part, A, W, S, s, fast_done);
+    else launch_mode<true, OUT_LOGP>(mode, part, A, W, S, s, fast_done);
   } else {
-    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, S, s, fast_done, fuse);
+    if (out_kind == OUT_SUM) launch_mode<false, OUT_SUM>(mode, part, A, W, S, s, fast_done);
     else if (out_kind == OUT_ARRAY)
-      launch_mode<false, OUT_ARRAY>(mode, part, A, W, S, s, fast_done, nullptr);
-    else launch_mode<false, OUT_LOGP>(mode, part, A, W, S, s, fast_done, nullptr);
+      launch_mode<false, OUT_ARRAY>(mode, part, A, W, S, s, fast_done);
+    else launch_mode<false, OUT_LOGP>(mode, part, A, W, S, s, fast_done);
   }
 }
 
@@ -2593,13 +2477,13 @@ int launch_small(const double* x, int64_t n, const Params& P, const Knobs& K, do
 void launch_finalize(const double* part, const int* zeros, int64_t nb, int defer_bits,
                      int* status, double* out, unsigned long long seq, hipStream_t s,
                      const int* split_rd, int* split_rs, int* tree_any, double* mirror,
-                     double* fin, int64_t fin_cap, int* ticket) {
-  const int64_t ng = (nb + 63) / 64;
-  const int64_t g = std::min<int64_t>(
-      kFinMaxBlocks, std::max<int64_t>(1, (ng + kFinGroupsPerBlock - 1) / kFinGroupsPerBlock));
+                     double* fin, int* ticket) {
+  int64_t g = 1;
+  if (fin && ticket && nb > 2 * kFinPerBlock)
+    g = std::min<int64_t>(kFinMaxBlocks, (nb + kFinPerBlock - 1) / kFinPerBlock);
   hipLaunchKernelGGL(finalize_kernel, dim3((unsigned)g), dim3(1024), 0, s, part, zeros, nb,
                      defer_bits, status, out, seq, split_rd, split_rs, tree_any, mirror, fin,
-                     fin_cap, ticket);
+                     ticket);
 }
 
 template <int MODE, bool COUNT>
@@ -2608,9 +2492,10 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                                   Params* d_par, int* n_defer, int* clist,
                                   unsigned long long* evals, int* status, int* prof,
                                   hipStream_t s, const NodeTables* nt) {
-  bool split = false;
+  bool split = false, spec = false;
   if constexpr ((MODE == kAdaptT || MODE == kAdaptTZ) && !COUNT) {
-    if (nt && nt->n_nodes > 0) {
+    spec = nt && nt->spec;
+    if (nt && nt->split && nt->n_nodes > 0) {
       // the call's node tables, then the t-node split level 0; the chunk
       // engine / records below read the device copy of the rows
       hipLaunchKernelGGL((node_split_kernel<MODE>), dim3((n + 63) / 64), dim3(kNodeSplit * 64), 0,
@@ -2630,7 +2515,7 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
                        n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof,
-                       split ? 1 : 0);
+                       spec ? 1 : 0);
   } else {
     // direct family: only exact-path records, one lane each
     const int64_t nl = (n + 63) / 64;

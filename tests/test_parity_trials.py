@@ -99,33 +99,42 @@ def test_node_terms_per_trial(gpu, oracle_lib, family):
     assert np.array_equal(ds.wiener_like_nodes(P, *KN), sums, equal_nan=True)
 
 
-@pytest.fixture(scope="module")
-def one_lane_ctx(gpu):
-    """A context whose per-node level 0 runs one lane per trial
-    (node_fast_kernel; WFPT_NODE_SPLIT=0), the reference point of the split."""
+def _ctx_env(env):
     import os
     from hddm_amd import _lib
-    old = os.environ.get("WFPT_NODE_SPLIT")
-    os.environ["WFPT_NODE_SPLIT"] = "0"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
-        ctx = _lib.Context(0)
+        return _lib.Context(0)
     finally:
-        if old is None:
-            del os.environ["WFPT_NODE_SPLIT"]
-        else:
-            os.environ["WFPT_NODE_SPLIT"] = old
-    yield ctx
-    ctx.close()
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.fixture(scope="module")
+def node_variant_ctxs(gpu):
+    """Contexts on the other node-path variants: the t-node split level 0
+    (WFPT_NODE_SPLIT=1) and the breadth-first rounds for sparse deferred
+    trials instead of the speculative records (WFPT_NODE_SPEC=0)."""
+    ctxs = {"split": _ctx_env({"WFPT_NODE_SPLIT": "1"}),
+            "rounds": _ctx_env({"WFPT_NODE_SPEC": "0"})}
+    yield ctxs
+    for c in ctxs.values():
+        c.close()
 
 
 @pytest.mark.parametrize("family", ["full", "heavy", "st_only", "c4_full"])
-def test_node_split_level0_bit_identical(gpu, oracle_lib, one_lane_ctx, family):
-    """The t-node split level 0 of the batched node call (node_grid_kernel +
-    node_split_kernel: five lanes per trial, the node tables built once per
-    call) gives every trial the bits of the one-lane-per-trial pass
-    (node_fast_kernel), per trial and per node, and it is the path the
-    default context takes (WFPT_PATH_NODE_SPLIT); per trial against the
-    reference at 1e-6."""
+def test_node_path_variants_bit_identical(gpu, oracle_lib, node_variant_ctxs, family):
+    """The batched node call's variants give every trial the same bits: the
+    default (one lane per trial at level 0, sparse deferred trials as
+    speculative records: node_record_spec evaluates every tree point in two
+    rounds and keeps the flags of the points the recursion reads), the t-node
+    split level 0 (node_split_kernel, five lanes per trial) and the
+    breadth-first records (node_records); per trial against the reference at
+    1e-6. The split context takes the split path (WFPT_PATH_NODE_SPLIT)."""
     from hddm_amd import _lib
     if family == "c4_full":
         from hddm_amd.hierarchical import HDDM, gen_data
@@ -140,19 +149,20 @@ def test_node_split_level0_bit_identical(gpu, oracle_lib, one_lane_ctx, family):
         rng = np.random.default_rng({"full": 11, "heavy": 12, "st_only": 13}[family])
         x, node, P = _node_dataset(rng, 57, family)
         kn = KN
-    out = []
-    for ctx in (_lib.context(), one_lane_ctx):
+    out = {}
+    for name, ctx in (("default", _lib.context()), ("split", node_variant_ctxs["split"]),
+                      ("rounds", node_variant_ctxs["rounds"])):
         ds = gpu.Dataset(x, node_id=node, n_nodes=P.shape[0], ctx=ctx)
         sums, terms = ds.wiener_like_nodes(P, *kn, trials=True)
-        split = bool(ctx.last_path() & _lib.PATH_NODE_SPLIT)
-        assert split == (ctx is not one_lane_ctx), family
+        assert bool(ctx.last_path() & _lib.PATH_NODE_SPLIT) == (name == "split"), (name, family)
         assert np.array_equal(ds.wiener_like_nodes(P, *kn), sums, equal_nan=True)
-        out.append((sums, terms))
+        out[name] = (sums, terms)
         ds.close()
-    assert np.array_equal(out[0][1], out[1][1], equal_nan=True), family
-    assert np.array_equal(out[0][0], out[1][0], equal_nan=True), family
+    for name in ("split", "rounds"):
+        assert np.array_equal(out["default"][1], out[name][1], equal_nan=True), (family, name)
+        assert np.array_equal(out["default"][0], out[name][0], equal_nan=True), (family, name)
     ref = node_terms_ref(oracle_lib, x, node, P, kn)
-    assert_logp_parity(out[0][1], ref, f"split {family}")
+    assert_logp_parity(out["default"][1], ref, f"node path {family}")
 
 
 @pytest.mark.parametrize("case", ["adapt_tz", "direct", "adapt_t", "adapt_z", "generic_sz",

@@ -13,7 +13,7 @@ import json; d=json.loads(open('$O/bench.log').read().strip().splitlines()[-1])
 print('bench', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'], 'stress', d['stress']['trials_per_s'], d['stress']['kernel_ms_avg'])"
 for sp in 0 1; do
   WFPT_NODE_SPLIT=$sp timeout -k 10 200 python -u tools/node_call_probe.py --reps 300 > $O/probe_${sp}.log 2>&1 || { echo "PROBE_FAIL rc=$?"; tail -5 $O/probe_${sp}.log; exit 1; }
-  cut -c1-200 $O/probe_${sp}.log
+  cut -c1-330 $O/probe_${sp}.log
   rm -rf $O/trace_$sp
   WFPT_NODE_SPLIT=$sp timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$sp -o t -- python3 tools/node_call_probe.py --reps 100 > $O/trace_$sp.log 2>&1 || { echo "TRACE_FAIL rc=$?"; exit 1; }
   python3 -c "

@@ -51,13 +51,19 @@ def main():
             for _ in range(50):
                 ds.wiener_like_nodes(T, **m.wp)
             ms, nl, _ = ctx.profile_read(reset=True)
+            ctx.profile(ctx.PROF_EVALS)  # one counting call: the deferred-trial tallies
+            ctx.profile_lists(reset=True)
+            ds.wiener_like_nodes(T, **m.wp)
+            lists = ctx.profile_lists(reset=True)
             ctx.profile(0)
             print(json.dumps({"full": full, "params": name,
                               "split": os.environ.get("WFPT_NODE_SPLIT", "1"),
                               "path": ctx.last_path(),
                               "call_us_median": float(np.median(ts)) * 1e6,
                               "call_us_p10": float(np.percentile(ts, 10)) * 1e6,
-                              "node_kernels_us": ms / nl * 1e3, "sum": float(np.sum(r))}),
+                              "node_kernels_us": ms / nl * 1e3, "sum": float(np.sum(r)),
+                              "deferred": lists.get("node_deferred"),
+                              "exact": lists.get("exact"), "walk": lists.get("walk")}),
                   flush=True)
 
 
