@@ -17,13 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
-    "s1d": ["WFPT_SMALL_2D=0"],
-    "nopf": ["WFPT_SIN_PREFETCH=0"],
-    # timing-only knockouts (wrong values): where the level-0 time goes
-    "ko_small": ["WFPT_KO_SMALL=1"],
-    "ko_large": ["WFPT_KO_LARGE=1"],
-    "ko_ldrift": ["WFPT_KO_LDRIFT=1"],
-    "ko_node": ["WFPT_KO_NODE=1"],
+    "exptab": ["WFPT_EXP_TABLE=1"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
