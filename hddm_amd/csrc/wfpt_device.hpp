@@ -986,12 +986,26 @@ __device__ const double kExp2J64[64] = {
     0x1.c199bdd85529cp+0, 0x1.c67f12e57d14bp+0, 0x1.cb720dcef9069p+0, 0x1.d072d4a07897cp+0,
     0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
     0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0};
+// WFPT_EXP_TABLE=2: the table read from LDS (each kernel copies it at entry:
+// exp_table_init), =1: from global memory
+#if WFPT_EXP_TABLE == 2
+__shared__ double sExp2J64[64];
+#define WFPT_EXP_TAB sExp2J64
+#else
+#define WFPT_EXP_TAB kExp2J64
+#endif
+__device__ inline void exp_table_init() {
+#if WFPT_EXP_TABLE == 2
+  for (int k = threadIdx.x; k < 64; k += blockDim.x) sExp2J64[k] = kExp2J64[k];
+  __syncthreads();
+#endif
+}
 __device__ inline double exp_val_tab(double x) {
   const double kd = rint(x * 92.33248261689366);  // 64 / ln2
   double r = fma(-kd, 0x1.62e42fefa39efp-7, x);  // ln2 / 64, two parts
   r = fma(-kd, 0x1.abc9e3b39803fp-62, r);
   const int k = (int)kd;
-  const double t = kExp2J64[k & 63];
+  const double t = WFPT_EXP_TAB[k & 63];
   double p = horner(0x1.1111111111111p-7, r, 0x1.5555555555555p-5);
   p = horner(p, r, 0x1.5555555555555p-3);
   p = horner(p, r, 0.5);

@@ -163,6 +163,7 @@ __device__ inline bool defer_slots(const Work& W, int64_t c, int lane, bool defe
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void fast_kernel(TrialArgs A, Work W) {
+  exp_table_init();
   const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
@@ -703,6 +704,7 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(TrialArgs A, Work W, EngTables tab,
                                                               Split S) {
+  exp_table_init();
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
@@ -865,6 +867,7 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
+  exp_table_init();
 #if WFPT_LEAN_REVERSE
   // blocks dispatched last take the first chunks (timing experiment)
   const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kFastBlock + threadIdx.x;
@@ -1015,6 +1018,7 @@ template <int MODE, bool COUNT, bool MULTI>
 __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
     const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
     const int* n_defer, unsigned long long* evals, int* status) {
+  exp_table_init();
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   node_records<MODE, COUNT, MULTI>(
@@ -1030,6 +1034,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_engine_kernel(
 // wave sum added to the chunk's partial (a fixed order).
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(256, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A, Work W, int64_t nw) {
+  exp_table_init();
   const int lane = threadIdx.x & 63;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   long long ne = 0;
@@ -1071,6 +1076,7 @@ __global__ __launch_bounds__(256, WFPT_SLOW_WAVES) void fold_kernel(TrialArgs A,
 // settle, per-block {sum, zeros} (OUT_SUM) or per-trial outputs.
 template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArgs A) {
+  exp_table_init();
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   long long ne = 0;
   double lp = 0.0;
@@ -1256,6 +1262,7 @@ struct FinArgs {
 template <int MODE, int OUT>
 __global__ __launch_bounds__(kFastBlock) void small_kernel(TrialArgs A, Work W, RootGrids R,
                                                            FinArgs F) {
+  exp_table_init();
   __shared__ double fp[kFastBlock / 64];
   __shared__ int fz[kFastBlock / 64];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -1392,6 +1399,7 @@ __device__ inline int l0_finish(const Trial& tr, const Params& P, const Knobs& K
 template <int MODE, int OUT>
 __global__ __launch_bounds__(kSplitBlock) void small_split_kernel(TrialArgs A, Work W,
                                                                  RootGrids R, FinArgs F) {
+  exp_table_init();
   static_assert(MODE == kAdaptTZ, "t-node split of the full DDM");
   __shared__ double sf[5][kFastBlock];  // t-node values, node-major
   __shared__ int sfl[kSplitLanes][kFastBlock];
@@ -1668,6 +1676,7 @@ template <int STK, bool COUNT>
 __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     unsigned long long* evals, int* status) {
+  exp_table_init();
   using Stack = typename StackOf<STK>::type;
   __shared__ Params rows[kStageRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
@@ -1713,6 +1722,7 @@ __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
                       double* lp, int64_t* d_idx, Params* d_par, int* n_defer, int* clist,
                       int* n_chunks, unsigned long long* evals, int* status, int* prof) {
+  exp_table_init();
   __shared__ Params rows[kStageRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
   const int64_t i = i0 + threadIdx.x;
@@ -1794,6 +1804,7 @@ template <int MODE>
 __global__ __launch_bounds__(kNodeSplit * 64) void node_split_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     int64_t* d_idx, Params* d_par, int* clist, int* n_chunks) {
+  exp_table_init();
   static_assert(MODE == kAdaptT || MODE == kAdaptTZ, "t-node split");
   __shared__ double sf[kNodeSplit][64];
   __shared__ int sfl[kNodeSplit][64];
@@ -2023,6 +2034,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
     unsigned long long* evals, int* status, int* prof, int spec) {
+  exp_table_init();
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
   ChunkLds<1>& cl = lds[threadIdx.x >> 6];
@@ -2152,6 +2164,7 @@ template <int MODE, int STK, bool COUNT, bool MULTI = false>
 __global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_slow_kernel(
     const double* x, Knobs K, double* lp, const int64_t* d_idx, const Params* d_par,
     const int* n_defer, unsigned long long* evals, int* status) {
+  exp_table_init();
   using Stack = typename StackOf<STK>::type;
   const int nd = *n_defer;
   long long ne = 0;
@@ -2180,6 +2193,7 @@ template <int STK>
 __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void multi_kernel(
     const double* x, int64_t n, const double* const* arr, const double* scal, Knobs K,
     double p_outlier, double* out, int* zeros, int* status, double* lpo) {
+  exp_table_init();
   using Stack = typename StackOf<STK>::type;
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   double lp = 0.0;
@@ -2242,6 +2256,7 @@ __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE
 void multi_fast_kernel(const double* x, int64_t n, const double* const* arr, const double* scal,
                        Knobs K, double p_outlier, double* lp, int64_t* d_idx, Params* d_par,
                        int* n_defer, unsigned long long* evals) {
+  exp_table_init();
   const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   long long ne = 0;

@@ -18,6 +18,7 @@ sys.path.insert(0, ROOT)
 VARIANTS = {
     "default": [],
     "exptab": ["WFPT_EXP_TABLE=1"],
+    "exptab_lds": ["WFPT_EXP_TABLE=2"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
