@@ -1753,13 +1753,19 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   const unsigned long long b = __ballot(defer);
   if (b) {
     if (MODE == kDirect) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(n_defer, __popcll(b));
-      base = __shfl(base, 0, 64);
+      // the rare exact-path trials settled on their own lane (node_slow_kernel's
+      // operations): no record, no second launch
       if (defer) {
-        const int k = base + __popcll(b & lanemask_lt(lane));
-        d_idx[k] = i;
-        d_par[k] = Q;
+        long long n1 = 0;
+        int f1 = 0;
+        const double xi = x[i];
+        double p = full_pdf<MODE, RegStack<2>>(xi, Q, K, n1, f1);
+        if (f1 & kFlagExact) p = __builtin_nan("");  // near-tie: settled exactly below
+        int fl = f1 & kFlagErrors;
+        p = settle(p, xi, Q, K, false, n1, fl);
+        if (fl & kFlagErrors) atomicOr(status, fl & kFlagErrors);
+        lp[i] = node_logp(p, Q, K);
+        if (COUNT) ne = n1;
       }
     } else {
       // the chunk for node_chunk_kernel and the trials as records for
@@ -1778,10 +1784,10 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
     }
   }
   if (COUNT) {
-    ne = wave_sum_ll(defer ? 0 : ne);
+    ne = wave_sum_ll((defer && MODE != kDirect) ? 0 : ne);
     if (lane == 0) {
       atomicAdd(evals, (unsigned long long)ne);
-      if (b) atomicAdd(&prof[3], __popcll(b));
+      if (b && MODE != kDirect) atomicAdd(&prof[3], __popcll(b));
     }
   }
 }
@@ -2531,13 +2537,8 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
                        n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof,
                        spec ? 1 : 0);
-  } else {
-    // direct family: only exact-path records, one lane each
-    const int64_t nl = (n + 63) / 64;
-    const int64_t g = nl < 64 ? nl : 64;  // rare exact-path records; kilobytes of scratch per lane
-    hipLaunchKernelGGL((node_slow_kernel<MODE, 0, COUNT>), dim3(g), dim3(64), 0, s, x, K, lp,
-                       d_idx, d_par, n_defer, evals, status);
   }
+  // direct family: node_fast_kernel settles its exact-path trials itself
 }
 
 template <bool COUNT>
