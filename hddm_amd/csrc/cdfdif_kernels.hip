@@ -103,6 +103,48 @@ __device__ inline void cdf_setup(const CdfPar& P, CdfShared& S) {
   __syncthreads();
 }
 
+// Lane l's value broadcast to the wave through scalar registers (a constant l:
+// two v_readlane_b32, no LDS round trip); WFPT_CDF_READLANE=0: __shfl.
+#ifndef WFPT_CDF_READLANE
+#define WFPT_CDF_READLANE 1
+#endif
+__device__ inline double bcast_lane(double v, int l) {
+#if WFPT_CDF_READLANE
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+#else
+  return __shfl(v, l, 64);
+#endif
+}
+
+// Lane base + k's value within a group of G lanes. G = 4 with WFPT_CDF_DPP:
+// a quad_perm DPP move per half (no LDS round trip), else __shfl.
+#ifndef WFPT_CDF_DPP
+#define WFPT_CDF_DPP 1
+#endif
+template <int K>
+__device__ inline double quad_bcast(double v) {
+  constexpr int ctrl = K | (K << 2) | (K << 4) | (K << 6);  // quad_perm [K, K, K, K]
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)b, ctrl, 0xF, 0xF, false);
+  const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), ctrl, 0xF, 0xF, false);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+template <int G>
+__device__ inline double group_bcast(double v, int base, int k) {
+  if (WFPT_CDF_DPP && G == 4) {
+    switch (k) {
+      case 0: return quad_bcast<0>(v);
+      case 1: return quad_bcast<1>(v);
+      case 2: return quad_bcast<2>(v);
+      default: return quad_bcast<3>(v);
+    }
+  }
+  return __shfl(v, base + k, 64);
+}
+
 // Series convergence test shared by the three series (cdfdif.c:144-146, 177-179, 202-204).
 __device__ inline bool converged(double h0, double h1, double h2) {
   return (fabs(h0 - h1) < kDelta) && (fabs(h1 - h2) < kDelta) && (h2 > 0);
@@ -209,11 +251,66 @@ __device__ inline double beyond_F(double h2, const CdfTrial& T, const CdfPar& P)
 // from the per-call table (window_terms, the same operations), past it they
 // are computed here.
 constexpr int kWinTerms = 512;
+#ifndef WFPT_CDF_CHUNK
+#define WFPT_CDF_CHUNK 8
+#endif
+constexpr int kWinChunk = WFPT_CDF_CHUNK;
+static_assert(kWinTerms % kWinChunk == 0 && kVMax % kWinChunk == 0, "kWinChunk");
 struct CdfWinTable {
   double vs[kWinTerms][2][6];  // v sin(sifa zzz(x, i))
   double dh[kWinTerms][6];     // -denom(v, m) / 2
   double l2[kWinTerms][6];     // 2 log(denom(v, m))
 };
+
+// The beyond-window factors for v < kBeyTerms in global memory, v fastest so
+// the wave kernel's 64 lanes (64 consecutive v) read them coalesced: its
+// series terms from one exp per drift node, the same operations as
+// beyond_term (bit-identical terms).
+constexpr int kBeyTerms = 512;
+#ifndef WFPT_CDF_BEY
+#define WFPT_CDF_BEY 1
+#endif
+struct CdfBeyTable {
+  double dh[6][kBeyTerms];       // -denom(v, m) / 2
+  double lx[6][kBeyTerms];       // log(1 - exp(dh * st_window))
+  double fact[2][6][kBeyTerms];  // fact(v, m) per boundary x
+};
+
+// The first kWinStage rows of the window table, staged into LDS by the wave
+// at its first window trial (one coalesced pass instead of a load round trip
+// per chunk of terms).
+constexpr int kWinStage = 64;
+static_assert(kWinStage % kWinChunk == 0 && kWinStage <= kWinTerms, "kWinStage");
+struct CdfWinStage {
+  double vs[kWinStage][2][6];
+  double dh[kWinStage][6];
+  double l2[kWinStage][6];
+};
+__device__ inline void stage_window(const CdfWinTable* __restrict__ W, CdfWinStage& L, int lane) {
+  const double* vs = &W->vs[0][0][0];
+  const double* dh = &W->dh[0][0];
+  const double* l2 = &W->l2[0][0];
+  double* lvs = &L.vs[0][0][0];
+  double* ldh = &L.dh[0][0];
+  double* ll2 = &L.l2[0][0];
+  // constant trip counts, so every load is issued before the first store
+  static_assert(kWinStage * 6 % 64 == 0, "stage rows");
+  double a[kWinStage * 12 / 64], b[kWinStage * 6 / 64], c[kWinStage * 6 / 64];
+#pragma unroll
+  for (int j = 0; j < kWinStage * 12 / 64; ++j) a[j] = vs[j * 64 + lane];
+#pragma unroll
+  for (int j = 0; j < kWinStage * 6 / 64; ++j) {
+    b[j] = dh[j * 64 + lane];
+    c[j] = l2[j * 64 + lane];
+  }
+#pragma unroll
+  for (int j = 0; j < kWinStage * 12 / 64; ++j) lvs[j * 64 + lane] = a[j];
+#pragma unroll
+  for (int j = 0; j < kWinStage * 6 / 64; ++j) {
+    ldh[j * 64 + lane] = b[j];
+    ll2[j * 64 + lane] = c[j];
+  }
+}
 
 __device__ inline double window_zzz(int x, int i, const CdfPar& P, const CdfShared& S) {
   const double gzi = S.gz[i];
@@ -228,7 +325,8 @@ __device__ inline double window_vs(int v, double zzz, double a) {
 }
 
 __device__ inline double window_mi(int m, int i, const CdfTrial& T, const CdfPar& P,
-                                   const CdfShared& S, const CdfWinTable* __restrict__ W) {
+                                   const CdfShared& S, const CdfWinTable* __restrict__ W,
+                                   const CdfWinStage& WS) {
   const double a = P.a, a2 = a * a, st = P.st, t = T.t, lower_t = T.lower_t;
   const int x = T.x, sg = T.sg, sh = T.sh;
   const double g = S.gk[m];
@@ -239,18 +337,41 @@ __device__ inline double window_mi(int m, int i, const CdfTrial& T, const CdfPar
                      ((((zzz * a2) / B) * cosh((((a - zzz) * sh) * g) / .01)) / sD);
   const double tl = t - lower_t;
   double h0 = 0, h1 = 0, h2 = 0;
-  for (int v = 0; v < kVMax; ++v) {
-    h0 = h1;
-    h1 = h2;
-    double term;
-    if (v < kWinTerms) {
-      term = W->vs[v][x][i] * exp((W->dh[v][m] * tl) - W->l2[v][m]);
+  // kWinChunk terms at a time: their loads and exps are independent, then they
+  // are added one by one with the test (terms past the stopping one are
+  // computed and dropped: the same partial sums and stopping term)
+  bool done = false;
+  for (int v0 = 0; v0 < kVMax && !done; v0 += kWinChunk) {
+    double term[kWinChunk];
+    if (v0 < kWinStage) {
+#pragma unroll
+      for (int u = 0; u < kWinChunk; ++u) {
+        const int v = v0 + u;
+        term[u] = WS.vs[v][x][i] * exp((WS.dh[v][m] * tl) - WS.l2[v][m]);
+      }
+    } else if (v0 < kWinTerms) {
+#pragma unroll
+      for (int u = 0; u < kWinChunk; ++u) {
+        const int v = v0 + u;
+        term[u] = W->vs[v][x][i] * exp((W->dh[v][m] * tl) - W->l2[v][m]);
+      }
     } else {
-      const double denom = window_denom(v, g, a2);
-      term = window_vs(v, zzz, a) * exp(((-.5 * denom) * tl) - (2 * log(denom)));
+#pragma unroll
+      for (int u = 0; u < kWinChunk; ++u) {
+        const int v = v0 + u;
+        const double denom = window_denom(v, g, a2);
+        term[u] = window_vs(v, zzz, a) * exp(((-.5 * denom) * tl) - (2 * log(denom)));
+      }
     }
-    h2 = h1 + term;
-    if (converged(h0, h1, h2)) break;
+#pragma unroll
+    for (int u = 0; u < kWinChunk; ++u) {
+      if (!done) {
+        h0 = h1;
+        h1 = h2;
+        h2 = h1 + term[u];
+        done = converged(h0, h1, h2);
+      }
+    }
   }
   return ((((.5 * S.w_g[i]) * (ser - (4 * h2))) * (kCPi / 100)) / (a2 * st)) *
          exp((((sg * zzz) * g) * 100));
@@ -265,15 +386,27 @@ __device__ inline double window_m0(const CdfTrial& T, const CdfPar& P) {
   const double sl = ((-(Z_L * Z_L)) / (12 * a2) + ((Z_L * Z_L) * Z_L) / ((12 * a) * a2)) -
                     ((((Z_L * Z_L) * Z_L) * Z_L) / ((48 * a2) * a2));
   double h0 = 0, h1 = 0, h2 = 0;
-  for (int v = 1; v < kVMax; ++v) {
-    h0 = h1;
-    h1 = h2;
-    const double sifa = (kCPi * v) / a;
-    const double denom = ((kCPi * v) * (kCPi * v)) / (a2 * 100);
-    h2 = h1 + (((1 / ((((((((kCPi * kCPi) * kCPi) * kCPi) * v) * v) * v) * v))) *
-                (cos(sifa * Z_L) - cos(sifa * Z_U))) *
-               exp((-.5 * denom) * (t - lower_t)));
-    if (converged(h0, h1, h2)) break;
+  bool done = false;  // v = 1 .. kVMax - 1 in chunks, as window_mi
+  for (int v0 = 0; v0 < kVMax && !done; v0 += kWinChunk) {
+    double term[kWinChunk];
+#pragma unroll
+    for (int u = 0; u < kWinChunk; ++u) {
+      const int v = v0 + u;
+      const double sifa = (kCPi * v) / a;
+      const double denom = ((kCPi * v) * (kCPi * v)) / (a2 * 100);
+      term[u] = ((1 / ((((((((kCPi * kCPi) * kCPi) * kCPi) * v) * v) * v) * v))) *
+                 (cos(sifa * Z_L) - cos(sifa * Z_U))) *
+                exp((-.5 * denom) * (t - lower_t));
+    }
+#pragma unroll
+    for (int u = 0; u < kWinChunk; ++u) {
+      if (!done && v0 + u >= 1) {
+        h0 = h1;
+        h1 = h2;
+        h2 = h1 + term[u];
+        done = converged(h0, h1, h2);
+      }
+    }
   }
   return (((400 * a2) * a) * ((sl - su) - h2)) / (st * sZ);
 }
@@ -303,10 +436,25 @@ struct CdfTable {
 // One block per drift node m, one lane per v: the parameter-only state
 // (cdf_setup) and the (v, m) factors of the beyond-window series.
 constexpr int kWinVsBlocks = kWinTerms * 12 / 64, kWinDenBlocks = kWinTerms * 6 / 64;
-constexpr int kCdfTableBlocks = 6 + kWinVsBlocks + kWinDenBlocks;
-__global__ __launch_bounds__(64) void cdf_table_kernel(CdfPar P, CdfTable* tab, CdfWinTable* W) {
+constexpr int kBeyBlocks = kBeyTerms * 6 / 64;
+constexpr int kCdfTableBlocks = 6 + kWinVsBlocks + kWinDenBlocks + kBeyBlocks;
+__global__ __launch_bounds__(64) void cdf_table_kernel(CdfPar P, CdfTable* tab, CdfWinTable* W,
+                                                       CdfBeyTable* B) {
   __shared__ CdfShared S;
   cdf_setup(P, S);
+  if (blockIdx.x >= 6 + kWinVsBlocks + kWinDenBlocks) {  // the wave kernel's beyond table
+    const int e = (blockIdx.x - (6 + kWinVsBlocks + kWinDenBlocks)) * 64 + threadIdx.x;
+    const int m = e / kBeyTerms, v = e % kBeyTerms;
+    const double a2 = P.a * P.a;
+    const double width = (P.Ter + (P.st / 2)) - (P.Ter - (P.st / 2));  // upper_t - lower_t
+    const double denom = beyond_denom(v, S.gk[m], a2);
+    const double dh = -.5 * denom;
+    B->dh[m][v] = dh;
+    B->lx[m][v] = beyond_lx(dh, width);
+    B->fact[0][m][v] = beyond_fact(v, m, 0, denom, P, S);
+    B->fact[1][m][v] = beyond_fact(v, m, 1, denom, P, S);
+    return;
+  }
   if (blockIdx.x >= 6) {  // the window series' tables
     const double a2 = P.a * P.a;
     const int b = blockIdx.x - 6;
@@ -384,7 +532,7 @@ __global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, i
       }
 #pragma unroll
       for (int k = 0; k < G; ++k) {
-        const double tk = G == 1 ? term : __shfl(term, base + k, 64);
+        const double tk = G == 1 ? term : group_bcast<G>(term, base, k);
         if (pend) {
           h0 = h1;
           h1 = h2;
@@ -420,12 +568,14 @@ __global__ __launch_bounds__(kCdfBlock) void dmat_cdf_kernel(const double* xs, i
 __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P,
                                                      const CdfTable* tab,
                                                      const CdfWinTable* __restrict__ W,
+                                                     const CdfBeyTable* __restrict__ B,
                                                      double p_outlier,
                                                      double w_outlier, double* out,
                                                      const int* defer, const int* n_defer) {
   const int nd = *n_defer;
   if ((int)blockIdx.x >= nd) return;
   __shared__ CdfShared S;
+  __shared__ CdfWinStage WS;
   {
     const double* src = (const double*)&tab->S;
     double* dst = (double*)&S;
@@ -434,11 +584,17 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
   }
   __syncthreads();
   const int lane = threadIdx.x;
+  bool staged = false;
   for (int k = blockIdx.x; k < nd; k += gridDim.x) {
     const int idx = defer[k];
     const double xi = xs[idx];
     const CdfTrial T = cdf_prepare(fabs(xi), xi > 0, P, S);
     double F;
+#ifdef WFPT_CDF_DEBUG
+    const long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
+    long long dbg_t1 = dbg_t0;
+    int dbg_rounds = 0;
+#endif
     if (T.branch == 1) {
       // h1, h2: the last two partial sums (the reference's sequential
       // additions, cdfdif.c:128-147). Per round the 64 additions run without
@@ -447,14 +603,48 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
       // series: the same sums and the same stopping term as one test per step.
       double h1 = 0, h2 = 0;
       bool conv = false;
+      // the table's factors of the next round are loaded one round ahead, so
+      // their latency overlaps this round's sequential additions
+      double qf[6], qd[6], ql[6];
+      const double* fx = &B->fact[T.x][0][0];
+#pragma unroll
+      for (int mm = 0; mm < 6; ++mm) {
+        qf[mm] = fx[mm * kBeyTerms + lane];
+        qd[mm] = B->dh[mm][lane];
+        ql[mm] = B->lx[mm][lane];
+      }
       for (int v0 = 0; v0 < kVMax && !conv; v0 += 64) {
         const int v = v0 + lane;
-        const double term = v < kVMax ? beyond_term(v, T, P, S) : 0.0;
+        double term = 0.0;
+        if (WFPT_CDF_BEY && v0 < kBeyTerms) {  // wave-uniform: kBeyTerms is a multiple of 64
+          double cf[6], cd[6], cx[6];
+#pragma unroll
+          for (int mm = 0; mm < 6; ++mm) {
+            cf[mm] = qf[mm];
+            cd[mm] = qd[mm];
+            cx[mm] = ql[mm];
+          }
+          if (v0 + 64 < kBeyTerms) {
+#pragma unroll
+            for (int mm = 0; mm < 6; ++mm) {
+              qf[mm] = fx[mm * kBeyTerms + v + 64];
+              qd[mm] = B->dh[mm][v + 64];
+              ql[mm] = B->lx[mm][v + 64];
+            }
+          }
+          const double t_up = T.t - T.upper_t;
+          double sum_nu = 0;
+#pragma unroll
+          for (int mm = 0; mm < 6; ++mm) sum_nu += cf[mm] * exp((cd[mm] * t_up) + cx[mm]);
+          term = v * sum_nu;
+        } else if (v < kVMax) {
+          term = beyond_term(v, T, P, S);
+        }
         const int m = (kVMax - v0 < 64) ? kVMax - v0 : 64;
         double h = h2, hk = 0.0;
 #pragma unroll
         for (int j = 0; j < 64; ++j) {
-          h = h + __shfl(term, j, 64);
+          h = h + bcast_lane(term, j);
           hk = lane == j ? h : hk;
         }
         const double up1 = __shfl(hk, (lane + 63) & 63, 64), up2 = __shfl(hk, (lane + 62) & 63, 64);
@@ -466,29 +656,49 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
         h1 = __shfl(hk, last > 0 ? last - 1 : 0, 64);
         if (last == 0) h1 = h2;
         h2 = __shfl(hk, last, 64);
+#ifdef WFPT_CDF_DEBUG
+        ++dbg_rounds;
+#endif
       }
       F = beyond_F(h2, T, P);
     } else {
+      if (!staged) {  // wave-uniform
+        stage_window(W, WS, lane);
+        __syncthreads();
+        staged = true;
+      }
       double val = 0.0;
       if (lane < 36) {
         const int m = lane / 6, i = lane % 6;
-        if (fabs(S.gk[m]) > kEps) val = window_mi(m, i, T, P, S, W);
+        if (fabs(S.gk[m]) > kEps) val = window_mi(m, i, T, P, S, W, WS);
       } else if (lane < 42) {
         if (!(fabs(S.gk[lane - 36]) > kEps)) val = window_m0(T, P);
       }
+#ifdef WFPT_CDF_DEBUG
+      dbg_t1 = __builtin_amdgcn_s_memrealtime();
+#endif
       double sum_nu = 0;
+#pragma unroll
       for (int m = 0; m < 6; ++m) {
         double sum_z = 0;
         if (fabs(S.gk[m]) > kEps) {
-          for (int i = 0; i < 6; ++i) sum_z += __shfl(val, m * 6 + i, 64);
+#pragma unroll
+          for (int i = 0; i < 6; ++i) sum_z += bcast_lane(val, m * 6 + i);
         } else {
-          sum_z = __shfl(val, 36 + m, 64);
+          sum_z = bcast_lane(val, 36 + m);
         }
         sum_nu += sum_z * S.w_gh[m];
       }
       F = ((T.p0 * (1 - T.x)) + (T.p1 * T.x)) - sum_nu;  // cdfdif.c:210
     }
     if (lane == 0) out[idx] = cdf_output(F, xi, p_outlier, w_outlier, S);
+#ifdef WFPT_CDF_DEBUG
+    // diagnostic builds: -(rounds 1e12 + series ticks 1e6 + elapsed ticks) in
+    // place of the value (100 MHz ticks from the trial's start)
+    if (lane == 0)
+      out[idx] = -((double)dbg_rounds * 1e12 + (double)(dbg_t1 - dbg_t0) * 1e6 +
+                   (double)(__builtin_amdgcn_s_memrealtime() - dbg_t0));
+#endif
   }
 }
 
@@ -499,13 +709,18 @@ __global__ __launch_bounds__(64) void cdf_wave_kernel(const double* xs, CdfPar P
 // (the per-call tables).
 // par holds the wrapper's transformed parameters (a/10, t, sv/10+1e-10,
 // z*a/10, sz*a/10+1e-10, st+1e-10, v/10).
+#ifndef WFPT_CDF_WAVES
+#define WFPT_CDF_WAVES 4096
+#endif
 #ifndef WFPT_CDF_GROUP
 #define WFPT_CDF_GROUP 4
 #endif
 // the buffer: CdfTable, then CdfWinTable at kCdfTableBeyond doubles
 constexpr int kCdfTableBeyond = 1344;
 static_assert(sizeof(CdfTable) <= kCdfTableBeyond * sizeof(double), "kCdfTableBeyond");
-static_assert(kCdfTableBeyond * sizeof(double) + sizeof(CdfWinTable) <=
+constexpr int kCdfTableWave = kCdfTableBeyond + 512 * 24;  // CdfBeyTable
+static_assert(sizeof(CdfWinTable) == 512 * 24 * sizeof(double), "CdfWinTable");
+static_assert(kCdfTableWave * sizeof(double) + sizeof(CdfBeyTable) <=
                   kCdfTableDoubles * sizeof(double), "kCdfTableDoubles");
 
 void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
@@ -522,7 +737,8 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   P.nu = par[6];
   CdfTable* T = reinterpret_cast<CdfTable*>(tab);
   CdfWinTable* W = reinterpret_cast<CdfWinTable*>(tab + kCdfTableBeyond);
-  hipLaunchKernelGGL(cdf_table_kernel, dim3(kCdfTableBlocks), dim3(64), 0, s, P, T, W);
+  CdfBeyTable* B = reinterpret_cast<CdfBeyTable*>(tab + kCdfTableWave);
+  hipLaunchKernelGGL(cdf_table_kernel, dim3(kCdfTableBlocks), dim3(64), 0, s, P, T, W, B);
   constexpr int G = WFPT_CDF_GROUP;
   const int64_t per_block = kCdfBlock / G;
   int64_t nb = (n + per_block - 1) / per_block;
@@ -530,9 +746,9 @@ void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_o
   hipLaunchKernelGGL(dmat_cdf_kernel<G>, dim3(nb), dim3(kCdfBlock), 0, s, x, n, P, T, p_outlier,
                      w_outlier, out, defer, n_defer);
   // one wave per deferred trial on a fixed grid (it reads the count itself)
-  const int64_t gw = n < 4096 ? n : 4096;
-  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, T, W, p_outlier, w_outlier,
-                     out, defer, n_defer);
+  const int64_t gw = n < WFPT_CDF_WAVES ? n : WFPT_CDF_WAVES;
+  hipLaunchKernelGGL(cdf_wave_kernel, dim3(gw), dim3(64), 0, s, x, P, T, W, B, p_outlier,
+                     w_outlier, out, defer, n_defer);
 }
 
 }  // namespace wfpt

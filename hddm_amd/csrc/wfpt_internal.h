@@ -171,7 +171,7 @@ void launch_multi(const double* x, int64_t n, const double* const* arr, const do
 // cdfdif_kernels.hip: dmat_cdf_array over device x[n]; par = the wrapper's
 // transformed (a, Ter, eta, z, sZ, st, nu) (cdfdif_wrapper.pyx:36-42).
 // defer: n ints of workspace, n_defer: one device int.
-constexpr int kCdfTableDoubles = 1344 + 512 * 24;  // per-call tables of launch_dmat_cdf
+constexpr int kCdfTableDoubles = 1344 + 512 * 48;  // per-call tables of launch_dmat_cdf
 void launch_dmat_cdf(const double* x, int64_t n, const double par[7], double p_outlier,
                      double w_outlier, double* out, double* tab, int* defer, int* n_defer,
                      hipStream_t s);
