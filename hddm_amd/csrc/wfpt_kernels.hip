@@ -864,15 +864,24 @@ __device__ inline ZGrid zgrid_uniform(const RootGrids& R, int b) {
 #define WFPT_SIN_TABLE 1
 #endif
 
+// Block size of the lean pass (WFPT_LEAN_BLOCK; its waves are independent:
+// one chunk each, no block-level exchange). The launch bound's second
+// argument is waves per SIMD (amdgpu_waves_per_eu), independent of the block
+// size, so the register budget is the same for every block size.
+#ifndef WFPT_LEAN_BLOCK
+#define WFPT_LEAN_BLOCK 256
+#endif
+constexpr int kLeanBlock = WFPT_LEAN_BLOCK;
+static_assert(kLeanBlock % 64 == 0 && kLeanBlock <= kFastBlock, "kLeanBlock");
 template <int MODE, bool COUNT, int OUT>
-__global__ __launch_bounds__(kFastBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
+__global__ __launch_bounds__(kLeanBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   exp_table_init();
 #if WFPT_LEAN_REVERSE
   // blocks dispatched last take the first chunks (timing experiment)
-  const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kFastBlock + threadIdx.x;
+  const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kLeanBlock + threadIdx.x;
 #else
-  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kLeanBlock + threadIdx.x;
 #endif
   const int lane = threadIdx.x & 63;
   const int64_t c = i >> 6;
@@ -2351,8 +2360,8 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
   } else if (lean) {
     RootGrids R;
     root_grids(A.P, R);
-    hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
-                       0, s, A, W, R);
+    hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3((A.n + kLeanBlock - 1) / kLeanBlock),
+                       dim3(kLeanBlock), 0, s, A, W, R);
   } else {
     const int64_t units = (int64_t)S.n * kSplit + (A.n + 63) / 64;
     hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>),

@@ -19,6 +19,8 @@ VARIANTS = {
     "default": [],
     "exptab": ["WFPT_EXP_TABLE=1"],
     "exptab_lds": ["WFPT_EXP_TABLE=2"],
+    "lb64": ["WFPT_LEAN_BLOCK=64"],
+    "lb128": ["WFPT_LEAN_BLOCK=128"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
@@ -64,10 +66,12 @@ print("RESULT " + json.dumps(res))
 '''
 
 
-def build():
+def build(names=None):
     from hddm_amd import build as hb
     os.makedirs(LIBDIR, exist_ok=True)
     for name, d in VARIANTS.items():
+        if names and name not in names:
+            continue
         hb.build(force=True, defines=d, out=os.path.join(LIBDIR, f"libwfpt_{name}.so"))
         print("built", name, flush=True)
 
@@ -102,7 +106,7 @@ def run(reps, names=None):
 
 if __name__ == "__main__":
     if sys.argv[1] == "build":
-        build()
+        build(sys.argv[sys.argv.index("--names") + 1].split(",") if "--names" in sys.argv else None)
     else:
         reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 3
         # --names a,b: time already-built hddm_amd/lib/variants/libwfpt_<name>.so
