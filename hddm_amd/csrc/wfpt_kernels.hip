@@ -1917,13 +1917,24 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
     if (lane == 0) lp[i] = node_logp(0.0, Q, K);
     return;
   }
+#ifdef WFPT_NODE_DEBUG
+  const long long dbg0 = __builtin_amdgcn_s_memrealtime();
+#endif
   eng_tables_wave(Q, T, lane);  // the record's tables in the wave's LDS
+#ifdef WFPT_NODE_DEBUG
+  wave_sync();
+  const long long dbg1 = __builtin_amdgcn_s_memrealtime();
+#endif
   const int flip = x0 > 0 ? 1 : 0;
   const double a = Q.a, sv = Q.sv;
   const double iwt = 1.0 / (T.tP[kTreeW] - T.tP[0]);
   const double ia2 = 1.0 / (a * a);  // as l0_hints / refine_rounds
   const L0Hints H = l0_hints(tr.x, T.tP[0], T.tP[kTreeW], a, K.err);
   const double izf = T.iz[flip];
+#ifdef WFPT_NODE_DEBUG3
+  long long dbgA = __builtin_amdgcn_s_memrealtime(), dbgB = 0, dbgC = 0, dbgD = 0;
+  int dbg_it = 0;
+#endif
   for (int e = lane; e < NE; e += 64) {
     int k, gs, jh = -1;
     if (e < NP * NG) {
@@ -1944,6 +1955,9 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
       kd = jh == 4 ? H.D4 : H.D0;
     }
     const TNode N = tnode_setup_r(tr.x - T.tP[k], tr.v, sv, a, ia2, K.err, qh, known, kd);
+#ifdef WFPT_NODE_DEBUG3
+    if (dbg_it == 0) dbgB = __builtin_amdgcn_s_memrealtime();
+#endif
     const int amb = N.amb ? (int)kFlagExact : 0;
     if (MODE == kAdaptT) {
       tv[k] = tnode_pdf_sv(N, tr.z, tr.v, sv, a) * iwt;
@@ -1962,8 +1976,18 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
         fh[jh] = amb | (ok ? 0 : kOvfBit);
       }
     }
+#ifdef WFPT_NODE_DEBUG3
+    if (dbg_it == 0) dbgC = __builtin_amdgcn_s_memrealtime();
+    ++dbg_it;
+#endif
   }
+#ifdef WFPT_NODE_DEBUG3
+  dbgD = __builtin_amdgcn_s_memrealtime();
+#endif
   wave_sync();
+#ifdef WFPT_NODE_DEBUG
+  const long long dbg2 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (MODE == kAdaptTZ && lane < NP) {
     // t point k's task completion (refine_rounds stage 0): the root test on
     // its root grid (hinted at level 0), then -- if it refines or the grid
@@ -2000,6 +2024,9 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
     fp[k] = flags;
   }
   wave_sync();
+#ifdef WFPT_NODE_DEBUG
+  const long long dbg3 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (lane == 0) {
     const double(&tk)[kTreePoints] = *reinterpret_cast<const double(*)[kTreePoints]>(tv);
     unsigned need = 0u, used = 0u;
@@ -2023,6 +2050,19 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
                                        : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
     }
     lp[i] = node_logp(p, Q, K);
+#ifdef WFPT_NODE_DEBUG
+    // diagnostic builds: the record's phase times (100 MHz ticks: tables,
+    // evaluations, z settlement, t tree + settlement) in place of its term
+    const long long dbg4 = __builtin_amdgcn_s_memrealtime();
+#ifdef WFPT_NODE_DEBUG3
+    // the evaluation phase instead: hints, first setup, first grid, the rest
+    lp[i] = -((double)(dbgA - dbg1) * 1e12 + (double)(dbgB - dbgA) * 1e8 +
+              (double)(dbgC - dbgB) * 1e4 + (double)(dbgD - dbgC));
+#else
+    lp[i] = -((double)(dbg1 - dbg0) * 1e12 + (double)(dbg2 - dbg1) * 1e8 +
+              (double)(dbg3 - dbg2) * 1e4 + (double)(dbg4 - dbg3));
+#endif
+#endif
   }
   wave_sync();  // the next record reuses the wave's LDS
 }
@@ -2062,6 +2102,9 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
       if (spec) {  // every tree point in two rounds (node_record_spec)
         int errf = 0;
         for (int k = w0; k < nrec; k += nwaves)
+#ifdef WFPT_NODE_DEBUG2
+          for (int dbg_rep = 0; dbg_rep < 2; ++dbg_rep)  // the second pass runs warm
+#endif
           node_record_spec<MODE>(cl.F, cl.X, cl.fl, cl.tab, lane, x, K, lp, r_idx[k], r_par[k],
                                  errf);  // F: 1088 doubles, fl: 64 ints
         if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);

@@ -19,6 +19,9 @@ VARIANTS = {
     "default": [],
     "exptab": ["WFPT_EXP_TABLE=1"],
     "exptab_lds": ["WFPT_EXP_TABLE=2"],
+    "nodedbg": ["WFPT_NODE_DEBUG"],
+    "nodedbg2": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG2"],
+    "nodedbg3": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG3"],
     "lb64": ["WFPT_LEAN_BLOCK=64"],
     "lb128": ["WFPT_LEAN_BLOCK=128"],
 }
