@@ -2013,6 +2013,94 @@ __host__ __device__ inline void root_grids(const Params& P, RootGrids& R) {
   }
 }
 
+// Per-call constants of the direct family (simple DDM: one pdf_sv per trial,
+// pdf.pxi:74-102 at w = z) for both boundaries, computed once on the host with
+// the device's operations (bit-identical): the flipped v and w (pdf.pxi:
+// 116-118), sin(pi w) and 2 cos(pi w) of the large-time series (tnode_ftt),
+// the drift exponent's trial-independent part (-v) a w, and 1 / a^2
+// (tnode_setup). `ok`: trial_setup's validity tests that do not involve x.
+struct DirectArgs {
+  double v[2], w[2], s1[2], tc[2], dn[2];
+  double ia2;
+  int ok;
+};
+__host__ __device__ inline void direct_args(const Params& P, DirectArgs& D) {
+  for (int b = 0; b < 2; ++b) {
+    const double v = b ? -P.v : P.v, w = b ? 1. - P.z : P.z;
+    D.v[b] = v;
+    D.w[b] = w;
+    double s1, c1;
+    sincospi01(w, s1, c1);
+    D.s1[b] = s1;
+    D.tc[b] = c1 + c1;
+    D.dn[b] = ((-v) * P.a) * w;
+  }
+  D.ia2 = 1.0 / (P.a * P.a);
+  const double a = P.a, sv = P.sv, t = P.t, st0 = P.st, sz0 = P.sz;
+  D.ok = !((P.z < 0) || (P.z > 1) || (a < 0) || (t < 0) || (st0 < 0) || (sv < 0) ||
+           (sz0 < 0) || (sz0 > 1) || (P.z + sz0 / 2. > 1) || (P.z - sz0 / 2. < 0) ||
+           (t - st0 / 2. < 0));
+}
+
+// tnode_ftt with the large-time sines given (DirectArgs): the same operations.
+__device__ inline double tnode_ftt_sc(const TNode& T, double w, double s1, double tc) {
+  double p = 0.0;
+  const int K = T.K;
+  if (T.small) {
+    const int lower = (int)(-floor((K - 1) / 2.));
+    const int upper = (int)ceil((K - 1) / 2.);
+    for (int k = lower; k <= upper; ++k) {
+      const double wk = w + (double)(2 * k);
+      p = madd(wk, exp_node((wk * wk) * T.m), p);
+    }
+    p = p * T.rn;
+  } else {
+    double sk = s1, skm1 = 0.0;
+    double e = T.m, r = T.m * T.q2;
+    if (K >= 1) p = e * s1;
+    for (int k = 2; k <= K; ++k) {
+      const double sn = msub(tc, sk, skm1);
+      skm1 = sk;
+      sk = sn;
+      e = e * r;
+      r = r * T.q2;
+      p = madd((double)k * e, sk, p);
+    }
+    p = p * kPi;
+  }
+  return p;
+}
+
+// fast_level0<kDirect> of a trial on boundary b with the call's DirectArgs:
+// the same operations (trial_setup's validity, tnode_setup, tnode_pdf_sv, the
+// settlement), with the trial-independent parts read from D.
+__device__ inline int direct_level0(double x0, const Params& P, const Knobs& K,
+                                    const DirectArgs& D, int b, double& p, long long& ne,
+                                    int& flags) {
+  p = 0.0;
+  const double x = fabs(x0);
+  if (!(D.ok && !((x - (P.t - P.st / 2.)) < 0))) return kFinal;
+  const double a = P.a, sv = P.sv, t = P.t;
+  const double v = D.v[b], w = D.w[b];
+  ne += 1;
+  const TNode T = tnode_setup_r(x - t, v, sv, a, D.ia2, K.err);
+  if (T.amb) flags |= kFlagExact;
+  if (T.pos) {
+    const double f = tnode_ftt_sc(T, w, D.s1[b], D.tc[b]);
+    if (sv == 0) {
+      const double ex = exp_node(D.dn[b] - (T.vvx * 0.5));
+      p = (f * ex) * T.sc;
+    } else {
+      p = tnode_pdf_sv(T, w, v, sv, a);  // (sv > 0: the general form)
+    }
+  }
+  if (flags & kFlagExact) return kExact;
+  if (p > kExactBelow || x - t <= 0) return kFinal;
+  if (!tiny_absorbed(p, P.p_outlier, K.w_outlier)) return kExact;
+  p = 0.0;
+  return kFinal;
+}
+
 // P(hit upper boundary), pdf.pxi:67-72
 __device__ inline double prob_ub(double v, double a, double z) {
   if (v == 0) return z;

@@ -191,6 +191,54 @@ void fast_kernel(TrialArgs A, Work W) {
   }
 }
 
+// The direct family's level-0 pass with the call's per-boundary constants
+// (DirectArgs: v, w, sin / 2cos(pi w), (-v) a w, 1 / a^2 computed once on the
+// host) instead of per-lane flips, sincospi and a division: the same outputs
+// as fast_kernel<kDirect> bit for bit (direct_level0). As in the lean pass, a
+// wave's trials are taken by boundary (datasets are ordered by boundary, then
+// |rt|), so the constants are wave-uniform; only the wave at the boundary
+// switch takes the second call site.
+#ifndef WFPT_DIRECT_ARGS
+#define WFPT_DIRECT_ARGS 1
+#endif
+template <bool COUNT, int OUT>
+__global__ __launch_bounds__(kFastBlock, FastWaves<kDirect>::value > 0 ? FastWaves<kDirect>::value : 1)
+void direct_kernel(TrialArgs A, Work W, DirectArgs D) {
+  exp_table_init();
+  const int64_t i = (int64_t)blockIdx.x * kFastBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int64_t c = i >> 6;
+  if (c * 64 >= A.n) return;  // a wave past the last chunk (wave-uniform)
+  const bool own = i < A.n;
+  const double x0 = own ? A.x[i] : 0.0;
+  double p = 0.0;
+  long long ne = 0;
+  int flags = 0, oc = kFinal;
+  const bool pos = x0 > 0;
+  const unsigned long long bo = __ballot(own), bp = __ballot(own && pos);
+  const int b = (bp == bo) ? 1 : 0;  // every trial upper: 1; otherwise lower first
+  if (own && pos == (b != 0)) oc = direct_level0(x0, A.P, A.K, D, b, p, ne, flags);
+  if (bp != 0ull && bp != bo) {  // mixed wave: its upper-boundary lanes
+    if (own && pos) oc = direct_level0(x0, A.P, A.K, D, 1, p, ne, flags);
+  }
+  double lp = 0.0;
+  int zero = 0;
+  if (own && oc == kFinal) emit<OUT>(A, i, p, lp, zero);
+  const bool anyd = defer_slots(W, c, lane, oc != kFinal, kFlagExact);
+  if (sum_out(OUT)) {
+    lp = wave_sum(lp);
+    const int zs = __popcll(__ballot(zero != 0));
+    if (lane == 0) {
+      A.out[c] = lp;
+      A.zeros[c] = zs | (anyd ? kZeroDefer : 0);
+    }
+  }
+  if (COUNT) {
+    const long long nf = wave_sum_ll(oc == kFinal ? ne : 0);
+    if (lane == 0) atomicAdd(A.evals, (unsigned long long)nf);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // The engine of the adaptive families (kAdaptT, kAdaptZ, kAdaptTZ;
 // integrate.pxi:72-206 driven by pdf.pxi:132-146). One wave owns a chunk of 64
@@ -2398,8 +2446,15 @@ template <int MODE, bool COUNT, int OUT>
 static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, const Split& S,
                      bool lean, hipStream_t s, hipEvent_t fast_done) {
   if constexpr (MODE == kDirect) {
-    hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock),
-                       0, s, A, W);
+    if (WFPT_DIRECT_ARGS) {
+      DirectArgs D;
+      direct_args(A.P, D);
+      hipLaunchKernelGGL((direct_kernel<COUNT, OUT>), dim3(fast_blocks(A.n)), dim3(kFastBlock), 0,
+                         s, A, W, D);
+    } else {
+      hipLaunchKernelGGL((fast_kernel<MODE, COUNT, OUT>), dim3(fast_blocks(A.n)),
+                         dim3(kFastBlock), 0, s, A, W);
+    }
   } else if (lean) {
     RootGrids R;
     root_grids(A.P, R);

@@ -22,6 +22,7 @@ VARIANTS = {
     "nodedbg": ["WFPT_NODE_DEBUG"],
     "nodedbg2": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG2"],
     "nodedbg3": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG3"],
+    "direct_off": ["WFPT_DIRECT_ARGS=0"],
     "lb64": ["WFPT_LEAN_BLOCK=64"],
     "lb128": ["WFPT_LEAN_BLOCK=128"],
 }
