@@ -312,10 +312,17 @@ struct ChunkLds {
   uint16_t ZQ[kQCap];                      // z walks of the level: owner | point << 6
 };
 
+// WFPT_SYNC_FENCE: wave_sync is also a scheduling barrier (experiment)
+#ifndef WFPT_SYNC_FENCE
+#define WFPT_SYNC_FENCE 0
+#endif
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#if WFPT_SYNC_FENCE
+  __builtin_amdgcn_sched_barrier(0);
+#endif
 }
 template <int TW>
 __device__ inline void team_sync() {
@@ -1947,13 +1954,70 @@ __global__ __launch_bounds__(kNodeSplit * 64) void node_split_kernel(
 // doubles: the walk values and the hinted root grids), tv (17 t values),
 // pf (>= 39 ints of point flags); lp[i] gets the node term.
 constexpr int kOvfBit = 1 << 8;  // a grid's drift factor overflowed (literal values)
-template <int MODE>
-__device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTables& T, int lane,
-                                        const double* x, const Knobs& K, double* lp, int64_t i,
-                                        const Params& Q, int& errf) {
+// The record's tables (eng_tables_wave's values) built by a team of NW waves:
+// with NW = 4 each wave computes one group (the 8 z grids, the t points, the
+// z points, the interval reciprocals), so the divergent groups run side by
+// side instead of one after another.
+template <int NW>
+__device__ inline void eng_tables_team(const Params& P, EngTables& T, int wave, int lane) {
+  if (NW == 1) {
+    eng_tables_wave(P, T, lane);
+    return;
+  }
+  constexpr int kP = kTreePoints;
+  if (wave == 0) {
+    if (lane < 8) {
+      const int flip = lane >> 2, sel = lane & 3;
+      const double zf = flip ? 1. - P.z : P.z, vf = flip ? -P.v : P.v;
+      T.G[flip][sel] = zgrid_of(zf - P.sz / 2., zf + P.sz / 2., sel, vf, P.sv, P.a);
+    }
+  } else if (wave == 1) {
+    if (lane < kP) T.tP[lane] = dyadic_point(P.t - P.st / 2., P.t + P.st / 2., lane);
+  } else if (wave == 2) {
+    if (lane < 2 * kP) {
+      const int flip = lane / kP, k = lane % kP;
+      const double zf = flip ? 1. - P.z : P.z;
+      T.zP[flip][k] = dyadic_point(zf - P.sz / 2., zf + P.sz / 2., k);
+    }
+  } else if (lane < 2) {
+    const int flip = lane;
+    const double zf = flip ? 1. - P.z : P.z;
+    T.iz[flip] = 1.0 / ((zf + P.sz / 2.) - (zf - P.sz / 2.));
+  }
+}
+// WFPT_REC_FENCE: a scheduling barrier between the record's phases. Without
+// them the compiler's schedule over the record's divergent phases makes the
+// call's records 1.5x slower (node_chunk_kernel 24.0 -> 15.6 us at config 4's
+// generating parameters, same code otherwise).
+#ifndef WFPT_REC_FENCES
+#define WFPT_REC_FENCES 1
+#endif
+#if WFPT_REC_FENCES
+#define WFPT_REC_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define WFPT_REC_FENCE() ((void)0)
+#endif
+template <int NW>
+__device__ inline void record_sync() {
+  if (NW == 1) wave_sync();
+  else __syncthreads();
+}
+// NW waves per record (NW = 1: the wave alone; NW = kEngWaves: the block,
+// every wave calling with the same record, wave = its index): the NE
+// evaluations are dealt to the waves in contiguous runs of t points, so each
+// wave's lanes take similar x - t (similar code paths: a round costs the
+// union of its lanes' paths), and the waves evaluate side by side. The
+// values, and so every output bit, are the same for any NW.
+template <int MODE, int NW>
+__device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTables& T, int wave,
+                                        int lane, const double* x, const Knobs& K, double* lp,
+                                        int64_t i, const Params& Q, int& errf,
+                                        long long dbg_entry = 0) {
   constexpr int NP = kTreePoints;
   constexpr int NG = MODE == kAdaptTZ ? 4 : 1;  // grids per t point
   constexpr int NE = NP * NG + (MODE == kAdaptTZ ? 5 : 0);
+  constexpr int kPer = (NE + NW - 1) / NW;  // evaluations per wave (NW > 1: one trip)
+  static_assert(NW == 1 || kPer <= 64, "record team");
   double* zv = buf;             // [NP][NP] the unhinted grids' values (the z walks)
   double* hv = buf + NP * NP;   // [5][5] the hinted root grids of the level-0 t points
   int* fu = pf;                 // [NP] unhinted root grid: kFlagExact (ambiguous) | kOvfBit
@@ -1962,28 +2026,30 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
   const double x0 = x[i];
   const Trial tr = trial_setup(x0, Q);
   if (!tr.valid) {  // (never deferred: p = 0 settles at level 0)
-    if (lane == 0) lp[i] = node_logp(0.0, Q, K);
+    if (wave == 0 && lane == 0) lp[i] = node_logp(0.0, Q, K);
     return;
   }
 #ifdef WFPT_NODE_DEBUG
   const long long dbg0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  eng_tables_wave(Q, T, lane);  // the record's tables in the wave's LDS
+  WFPT_REC_FENCE();
+  eng_tables_team<NW>(Q, T, wave, lane);  // the record's tables in LDS
+  record_sync<NW>();
 #ifdef WFPT_NODE_DEBUG
-  wave_sync();
   const long long dbg1 = __builtin_amdgcn_s_memrealtime();
 #endif
+  WFPT_REC_FENCE();
   const int flip = x0 > 0 ? 1 : 0;
   const double a = Q.a, sv = Q.sv;
   const double iwt = 1.0 / (T.tP[kTreeW] - T.tP[0]);
   const double ia2 = 1.0 / (a * a);  // as l0_hints / refine_rounds
   const L0Hints H = l0_hints(tr.x, T.tP[0], T.tP[kTreeW], a, K.err);
   const double izf = T.iz[flip];
-#ifdef WFPT_NODE_DEBUG3
-  long long dbgA = __builtin_amdgcn_s_memrealtime(), dbgB = 0, dbgC = 0, dbgD = 0;
-  int dbg_it = 0;
-#endif
-  for (int e = lane; e < NE; e += 64) {
+  const int e_lo = NW == 1 ? 0 : wave * kPer;
+  const int e_hi = NW == 1 ? NE : ((wave + 1) * kPer < NE ? (wave + 1) * kPer : NE);
+  for (int e0 = e_lo; e0 < e_hi; e0 += 64) {
+    const int e = e0 + lane;
+    if (e >= e_hi) continue;
     int k, gs, jh = -1;
     if (e < NP * NG) {
       k = e / NG;
@@ -2003,9 +2069,6 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
       kd = jh == 4 ? H.D4 : H.D0;
     }
     const TNode N = tnode_setup_r(tr.x - T.tP[k], tr.v, sv, a, ia2, K.err, qh, known, kd);
-#ifdef WFPT_NODE_DEBUG3
-    if (dbg_it == 0) dbgB = __builtin_amdgcn_s_memrealtime();
-#endif
     const int amb = N.amb ? (int)kFlagExact : 0;
     if (MODE == kAdaptT) {
       tv[k] = tnode_pdf_sv(N, tr.z, tr.v, sv, a) * iwt;
@@ -2024,19 +2087,13 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
         fh[jh] = amb | (ok ? 0 : kOvfBit);
       }
     }
-#ifdef WFPT_NODE_DEBUG3
-    if (dbg_it == 0) dbgC = __builtin_amdgcn_s_memrealtime();
-    ++dbg_it;
-#endif
   }
-#ifdef WFPT_NODE_DEBUG3
-  dbgD = __builtin_amdgcn_s_memrealtime();
-#endif
-  wave_sync();
+  record_sync<NW>();
 #ifdef WFPT_NODE_DEBUG
   const long long dbg2 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (MODE == kAdaptTZ && lane < NP) {
+  WFPT_REC_FENCE();
+  if (MODE == kAdaptTZ && wave == 0 && lane < NP) {
     // t point k's task completion (refine_rounds stage 0): the root test on
     // its root grid (hinted at level 0), then -- if it refines or the grid
     // overflowed -- the z walk over the unhinted grids
@@ -2071,11 +2128,12 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
     tv[k] = val;
     fp[k] = flags;
   }
-  wave_sync();
+  if (wave == 0) wave_sync();
 #ifdef WFPT_NODE_DEBUG
   const long long dbg3 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (lane == 0) {
+  WFPT_REC_FENCE();
+  if (wave == 0 && lane == 0) {
     const double(&tk)[kTreePoints] = *reinterpret_cast<const double(*)[kTreePoints]>(tv);
     unsigned need = 0u, used = 0u;
     int fl = 0, nref = 0;
@@ -2098,21 +2156,19 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
                                        : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
     }
     lp[i] = node_logp(p, Q, K);
-#ifdef WFPT_NODE_DEBUG
+#if defined(WFPT_NODE_DEBUG) && !defined(WFPT_NODE_DEBUG_NOOUT)
     // diagnostic builds: the record's phase times (100 MHz ticks: tables,
     // evaluations, z settlement, t tree + settlement) in place of its term
     const long long dbg4 = __builtin_amdgcn_s_memrealtime();
-#ifdef WFPT_NODE_DEBUG3
-    // the evaluation phase instead: hints, first setup, first grid, the rest
-    lp[i] = -((double)(dbgA - dbg1) * 1e12 + (double)(dbgB - dbgA) * 1e8 +
-              (double)(dbgC - dbgB) * 1e4 + (double)(dbgD - dbgC));
-#else
     lp[i] = -((double)(dbg1 - dbg0) * 1e12 + (double)(dbg2 - dbg1) * 1e8 +
               (double)(dbg3 - dbg2) * 1e4 + (double)(dbg4 - dbg3));
+#ifdef WFPT_NODE_DEBUG_ENTRY
+    // the kernel's entry -> record start and the record's total instead
+    lp[i] = -((double)(dbg0 - dbg_entry) * 1e8 + (double)(dbg4 - dbg0));
 #endif
 #endif
   }
-  wave_sync();  // the next record reuses the wave's LDS
+  record_sync<NW>();  // the next record reuses the LDS
 }
 
 // The node path's completion of the chunks node_fast_kernel listed: one wave
@@ -2132,11 +2188,21 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
 // fast pass's records one wave each instead (node_records), which skips the
 // level 0 of the chunks' settled trials. Trials the rounds hand on (the exact
 // path, trees deeper than kTreeDepth) are settled on their own lane (rare).
+// WFPT_NODE_REC_TEAM: a speculative record is one block's work (its waves
+// evaluate side by side), else one wave's.
+#ifndef WFPT_NODE_REC_TEAM
+#define WFPT_NODE_REC_TEAM 1
+#endif
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
     unsigned long long* evals, int* status, int* prof, int spec) {
+#ifdef WFPT_NODE_DEBUG
+  const long long dbg_entry = __builtin_amdgcn_s_memrealtime();
+#else
+  const long long dbg_entry = 0;
+#endif
   exp_table_init();
   __shared__ ChunkLds<1> lds[kEngWaves];
   const int lane = threadIdx.x & 63;
@@ -2149,12 +2215,18 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     if constexpr (!COUNT && (MODE == kAdaptT || MODE == kAdaptTZ)) {
       if (spec) {  // every tree point in two rounds (node_record_spec)
         int errf = 0;
-        for (int k = w0; k < nrec; k += nwaves)
-#ifdef WFPT_NODE_DEBUG2
-          for (int dbg_rep = 0; dbg_rep < 2; ++dbg_rep)  // the second pass runs warm
-#endif
-          node_record_spec<MODE>(cl.F, cl.X, cl.fl, cl.tab, lane, x, K, lp, r_idx[k], r_par[k],
-                                 errf);  // F: 1088 doubles, fl: 64 ints
+        if (WFPT_NODE_REC_TEAM) {
+          // one block per record, its waves side by side (wave 0's LDS)
+          ChunkLds<1>& c0 = lds[0];
+          const int wv = threadIdx.x >> 6;
+          for (int k = (int)blockIdx.x; k < nrec; k += (int)gridDim.x)
+            node_record_spec<MODE, kEngWaves>(c0.F, c0.X, c0.fl, c0.tab, wv, lane, x, K, lp,
+                                              r_idx[k], r_par[k], errf, dbg_entry);
+        } else {
+          for (int k = w0; k < nrec; k += nwaves)
+            node_record_spec<MODE, 1>(cl.F, cl.X, cl.fl, cl.tab, 0, lane, x, K, lp, r_idx[k],
+                                      r_par[k], errf, dbg_entry);  // F: 1088 doubles, fl: 64 ints
+        }
         if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
         return;
       }

@@ -20,8 +20,12 @@ VARIANTS = {
     "exptab": ["WFPT_EXP_TABLE=1"],
     "exptab_lds": ["WFPT_EXP_TABLE=2"],
     "nodedbg": ["WFPT_NODE_DEBUG"],
-    "nodedbg2": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG2"],
-    "nodedbg3": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG3"],
+    "nodedbg_solo": ["WFPT_NODE_DEBUG", "WFPT_NODE_REC_TEAM=0"],
+    "nodedbg_entry": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG_ENTRY"],
+    "stamps_noout": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG_NOOUT"],
+    "recfence": ["WFPT_REC_FENCES=1"],
+    "syncfence": ["WFPT_SYNC_FENCE=1"],
+    "rec_solo": ["WFPT_NODE_REC_TEAM=0"],
     "direct_off": ["WFPT_DIRECT_ARGS=0"],
     "lb64": ["WFPT_LEAN_BLOCK=64"],
     "lb128": ["WFPT_LEAN_BLOCK=128"],

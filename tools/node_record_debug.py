@@ -32,6 +32,13 @@ def main():
         _, terms = ds.wiener_like_nodes(P, trials=True, **m.wp)
     d = np.flatnonzero(terms < -1e3)
     print("records", d.size)
+    if os.environ.get("ENTRY"):  # WFPT_NODE_DEBUG_ENTRY build
+        for k in d:
+            v = -terms[k]
+            e = np.floor(v / 1e8 + 1e-9)
+            print("  trial", int(k), "kernel entry -> record start %.2f us, record %.2f us" %
+                  (e / 100, (v - e * 1e8) / 100))
+        return
     for k in d:
         v = -terms[k]
         f = []
