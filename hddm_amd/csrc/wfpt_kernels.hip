@@ -1645,16 +1645,22 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
 }
 
 // segment_sum_kernel's per-node sums and publish_nodes_kernel's publication in
-// one launch: each node's wave writes its sum straight to the mapped slot
-// (fine-grained host memory: uncached, so the store's completion, which every
-// wave waits for, is its visibility) and its block adds to an agent-scope
-// ticket; the last block writes the encoded error flags and, after a system
-// fence, the completion word, and resets the call's counters (the node path's
+// one launch: each node's wave writes its sum to the device vector res, its
+// block releases them and adds to an agent-scope ticket; the last block
+// copies the sums to the mapped slot, writes the encoded error flags and,
+// after a system fence, the completion word, and resets the call's counters
+// (r05: the waves' direct writes to the mapped slot, ordered only by their
+// own completion, once let the completion word overtake a node's sum; the
+// node path's
 // n_defer words and the ticket: 0 at rest, stream order).
+#ifndef WFPT_PUB_WT
+#define WFPT_PUB_WT 1
+#endif
 __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, const int64_t* off,
                                                               int32_t n_nodes, int* status,
-                                                              double* out, unsigned long long seq,
-                                                              int* ticket, int* counters) {
+                                                              double* res, double* out,
+                                                              unsigned long long seq, int* ticket,
+                                                              int* counters) {
   __shared__ int last;
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -1669,24 +1675,47 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
     }
     s = wave_sum(s);
     const bool anyz = __ballot(zero != 0) != 0ull;
-    if (lane == 0) out[j] = anyz ? -INFINITY : s;
+    if (lane == 0) {
+#if WFPT_PUB_WT
+      __hip_atomic_store(&res[j], anyz ? -INFINITY : s, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+#else
+      res[j] = anyz ? -INFINITY : s;
+#endif
+    }
   }
+  // device-memory sums made visible at agent scope before the block's ticket
+  // (WFPT_PUB_WT: agent-coherent stores, waited for; else finalize_kernel's
+  // release fence); the last block alone writes the mapped slot, so one
+  // thread order + one system fence precede the completion word
+#if WFPT_PUB_WT
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
   __syncthreads();
   if (threadIdx.x == 0)
     last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
            (int)gridDim.x - 1;
   __syncthreads();
-  if (!last || threadIdx.x != 0) return;
-  *ticket = 0;
-  counters[0] = 0;
-  counters[1] = 0;
-  counters[2] = 0;
-  const int st = atomicExch(status, 0);
-  out[n_nodes] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int k = threadIdx.x; k < n_nodes; k += 256)
+    out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    *ticket = 0;
+    counters[0] = 0;
+    counters[1] = 0;
+    counters[2] = 0;
+    const int st = atomicExch(status, 0);
+    out[n_nodes] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
+  }
   __threadfence_system();
-  reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
-  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
+    __threadfence_system();
+  }
 }
 
 // Node all-reduce (wfpt_wiener_like_nodes_allreduce): the encoded error
@@ -1727,6 +1756,12 @@ __global__ __launch_bounds__(256) void publish_vec_kernel(const double* res, int
 // reads its row there. Blocks spanning more than kStageRows ids (empty nodes
 // between) read the table directly.
 constexpr int kStageRows = 256;
+// node_fast_kernel: root grids staged per block for up to this many nodes
+// (WFPT_NODE_L0T; a block of 256 stored trials spans 2 HDDM nodes of 250)
+#ifndef WFPT_NODE_L0T
+#define WFPT_NODE_L0T 0
+#endif
+constexpr int kNodeGridRows = 4;
 
 template <int STK>
 struct StackOf {
@@ -1788,6 +1823,7 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
                       int* n_chunks, unsigned long long* evals, int* status, int* prof) {
   exp_table_init();
   __shared__ Params rows[kStageRows];
+  __shared__ RootGrids grids[kNodeGridRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
   const int64_t i = i0 + threadIdx.x;
   const int lane = threadIdx.x & 63;
@@ -1801,6 +1837,15 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
     for (int k = threadIdx.x; k < span * 8; k += kBlock) dst[k] = src[k];
   }
   __syncthreads();
+  // the full DDM with few nodes per block: each staged node's root z grids and
+  // sine tables once per block (root_grids: the engine's zgrid_of operations),
+  // and the lean pass's level 0 over them (eng_level0_t, the same bits as the
+  // engine's level 0) instead of a grid set up per lane
+  const bool gridded = WFPT_NODE_L0T && MODE == kAdaptTZ && staged && span <= kNodeGridRows;
+  if (gridded) {
+    if ((int)threadIdx.x < span) root_grids(rows[threadIdx.x], grids[threadIdx.x]);
+    __syncthreads();
+  }
   long long ne = 0;
   bool defer = false;
   Params Q;
@@ -1810,7 +1855,16 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
     double p, f[5];
     int flags = 0;
     unsigned pend;
-    const int oc = fast_level0<MODE>(x[i], Q, K, p, f, ne, flags, pend);
+    int oc;
+    if (gridded) {
+      const double xi = x[i];
+      const bool flip = xi > 0;
+      const RootGrids& R = grids[nj - first];
+      oc = eng_level0_t<MODE, false, true>(trial_setup_b(xi, Q, flip), Q, K, R.G[flip], p, f, ne,
+                                           pend, WFPT_SIN_TABLE ? &R.S[flip][0][0] : nullptr);
+    } else {
+      oc = fast_level0<MODE>(x[i], Q, K, p, f, ne, flags, pend);
+    }
     if (oc == kFinal) lp[i] = node_logp(p, Q, K);
     else defer = true;
   }
@@ -2791,9 +2845,8 @@ void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, d
                         double* out, int* status, unsigned long long seq, hipStream_t s,
                         int* ticket, int* counters) {
   if (n_nodes <= 0) return;
-  (void)res;
   hipLaunchKernelGGL(segment_publish_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                     n_nodes, status, out, seq, ticket, counters);
+                     n_nodes, status, res, out, seq, ticket, counters);
 }
 
 template <int MODE, bool COUNT>

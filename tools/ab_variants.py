@@ -25,6 +25,7 @@ VARIANTS = {
     "stamps_noout": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG_NOOUT"],
     "recfence": ["WFPT_REC_FENCES=1"],
     "syncfence": ["WFPT_SYNC_FENCE=1"],
+    "pub_fence": ["WFPT_PUB_WT=0"],
     "ilp": ["-mllvm -amdgpu-sched-strategy=max-ilp"],
     "latbias": ["-mllvm -amdgpu-schedule-metric-bias=0"],
     "rec_solo": ["WFPT_NODE_REC_TEAM=0"],
