@@ -527,3 +527,36 @@ def test_rccl_node_allreduce_failure_paths(gpu, monkeypatch):
                                                _lib.dptr(out))
     assert rc == 2
     assert np.array_equal(ds.wiener_like_nodes_allreduce(params), want)
+
+
+def test_bench_launcher_does_not_touch_gpu():
+    """bench.py --gpus N without a torch.distributed environment starts
+    torch.distributed.run with N ranks on 127.0.0.1 before loading the library
+    or anything that initialises a GPU (a process that has touched the GPU
+    must not hand over to another program on this pool)."""
+    import subprocess
+    import sys
+    code = (
+        "import atexit, os, sys\n"
+        "os.environ.pop('WORLD_SIZE', None)\n"
+        "sys.path.insert(0, %r)\n"
+        "import bench\n"
+        "seen = []\n"
+        "bench.subprocess.call = lambda cmd: seen.append(cmd) or 0\n"
+        "sys.argv = ['bench.py', '--gpus', '8', '--steps', '2']\n"
+        "try:\n"
+        "    bench.main()\n"
+        "except SystemExit as e:\n"
+        "    assert e.code == 0, e.code\n"
+        "loaded = sorted(m for m in sys.modules if m.startswith('hddm_amd') or m.startswith('torch'))\n"
+        "print('CMD', seen[0])\n"
+        "print('LOADED', loaded)\n" % ROOT)
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    cmd = next(l for l in r.stdout.splitlines() if l.startswith("CMD"))
+    loaded = next(l for l in r.stdout.splitlines() if l.startswith("LOADED"))
+    assert "torch.distributed.run" in cmd and "--nproc-per-node=8" in cmd
+    assert "--master-addr=127.0.0.1" in cmd
+    assert loaded == "LOADED []", loaded
