@@ -1821,6 +1821,9 @@ __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
                       double* lp, int64_t* d_idx, Params* d_par, int* n_defer, int* clist,
                       int* n_chunks, unsigned long long* evals, int* status, int* prof) {
+#ifdef WFPT_NODE_DEBUG_FAST
+  const long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
   exp_table_init();
   __shared__ Params rows[kStageRows];
   __shared__ RootGrids grids[kNodeGridRows];
@@ -1901,6 +1904,12 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
       }
     }
   }
+#ifdef WFPT_NODE_DEBUG_FAST
+  // diagnostic builds: lane 0's term of every wave is replaced by
+  // -(1e6 + the wave's elapsed 100 MHz ticks) (tools/node_fast_debug.py)
+  if (lane == 0 && i < n)
+    lp[i] = -(1e6 + (double)(__builtin_amdgcn_s_memrealtime() - dbg_t0));
+#endif
   if (COUNT) {
     ne = wave_sum_ll((defer && MODE != kDirect) ? 0 : ne);
     if (lane == 0) {

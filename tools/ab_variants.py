@@ -26,6 +26,7 @@ VARIANTS = {
     "recfence": ["WFPT_REC_FENCES=1"],
     "syncfence": ["WFPT_SYNC_FENCE=1"],
     "pub_fence": ["WFPT_PUB_WT=0"],
+    "fastdbg": ["WFPT_NODE_DEBUG_FAST"],
     "ilp": ["-mllvm -amdgpu-sched-strategy=max-ilp"],
     "latbias": ["-mllvm -amdgpu-schedule-metric-bias=0"],
     "rec_solo": ["WFPT_NODE_REC_TEAM=0"],
