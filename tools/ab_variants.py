@@ -28,6 +28,9 @@ VARIANTS = {
     "pub_fence": ["WFPT_PUB_WT=0"],
     "fastdbg": ["WFPT_NODE_DEBUG_FAST"],
     "ilp": ["-mllvm -amdgpu-sched-strategy=max-ilp"],
+    "occbias": ["-mllvm -amdgpu-schedule-metric-bias=100"],
+    "memclause": ["-mllvm -amdgpu-sched-strategy=max-memory-clause"],
+    "wavepri": ["-mllvm -amdgpu-set-wave-priority"],
     "latbias": ["-mllvm -amdgpu-schedule-metric-bias=0"],
     "rec_solo": ["WFPT_NODE_REC_TEAM=0"],
     "direct_off": ["WFPT_DIRECT_ARGS=0"],
