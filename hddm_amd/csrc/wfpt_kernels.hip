@@ -1656,6 +1656,12 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
 #ifndef WFPT_PUB_WT
 #define WFPT_PUB_WT 1
 #endif
+// WFPT_PUB_DIRECT=1 (diagnostic builds only): each wave writes its node's sum
+// straight to the mapped slot, as r05 first did (test_node_sums_never_stale
+// is the check that catches it)
+#ifndef WFPT_PUB_DIRECT
+#define WFPT_PUB_DIRECT 0
+#endif
 __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, const int64_t* off,
                                                               int32_t n_nodes, int* status,
                                                               double* res, double* out,
@@ -1676,7 +1682,9 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
     s = wave_sum(s);
     const bool anyz = __ballot(zero != 0) != 0ull;
     if (lane == 0) {
-#if WFPT_PUB_WT
+#if WFPT_PUB_DIRECT
+      out[j] = anyz ? -INFINITY : s;  // (diagnostic: the racy r05 form, tests only)
+#elif WFPT_PUB_WT
       __hip_atomic_store(&res[j], anyz ? -INFINITY : s, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
 #else
@@ -1700,8 +1708,9 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
   __syncthreads();
   if (!last) return;
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  for (int k = threadIdx.x; k < n_nodes; k += 256)
-    out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!WFPT_PUB_DIRECT)
+    for (int k = threadIdx.x; k < n_nodes; k += 256)
+      out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x == 0) {
     *ticket = 0;
     counters[0] = 0;

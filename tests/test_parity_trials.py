@@ -488,3 +488,36 @@ def test_node_dataset_with_nan_rts(gpu, oracle_lib, family):
             assert np.isnan(sums[j]), j
         elif tj.size:
             assert abs(sums[j] - math.fsum(tj)) <= 1e-12 * math.fsum(np.abs(tj)) + 1e-12, j
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("full", [False, True])
+def test_node_sums_never_stale(gpu, full):
+    """The batched node call's per-node sums reach the mapped result slot
+    before its completion word. r05 first had every node's wave write its sum
+    straight to the slot; one full GPU-suite run then read a node sum of the
+    previous call. The publication now has a single writer and a system fence
+    before the word. This loop is the regression guard: alternating two
+    parameter tables, every call must return exactly the sums of its own
+    table (it did not reproduce the rare race on the old build in 550 calls:
+    a guard, not a proof)."""
+    from hddm_amd.hierarchical import HDDM, gen_data
+    inter = dict(sv=0.1, sz=0.1, st=0.1) if full else {}
+    data, truth = gen_data(n_subj=200, n_trials=500, **inter)
+    m = HDDM(data, depends_on={"v": "cond"}, include=tuple(inter), p_outlier=0.05)
+    A = m.node_table()
+    B = A.copy()
+    for j, (s, c) in enumerate(m.node_keys):
+        B[j, 0] = truth["v"][c][s]
+        B[j, 2] = truth["a"][s]
+        B[j, 5] = truth["t"][s]
+    ds = m.dataset
+    ra = ds.wiener_like_nodes(A, **m.wp).copy()
+    rb = ds.wiener_like_nodes(B, **m.wp).copy()
+    assert not np.array_equal(ra, rb)
+    reps = 150 if full else 400
+    for k in range(reps):
+        T, ref = (A, ra) if k % 2 == 0 else (B, rb)
+        r = ds.wiener_like_nodes(T, **m.wp)
+        bad = np.flatnonzero(r != ref)
+        assert bad.size == 0, (k, bad[:5], r[bad[:5]], ref[bad[:5]])
