@@ -76,6 +76,18 @@ wfpt_shard_range = _sig("wfpt_shard_range", None,
 wfpt_wiener_like = _sig("wfpt_wiener_like", _I, [_VP, _VP, _PP, _PK, _PD])
 wfpt_wiener_like_host = _sig("wfpt_wiener_like_host", _I, [_VP, _PD, _I64, _PP, _PK, _PD])
 wfpt_wiener_like_nodes = _sig("wfpt_wiener_like_nodes", _I, [_VP, _VP, _PP, _PK, _PD])
+
+
+def _raw(name, nargs):
+    """The same entry point through a prototype of plain addresses (ints): the
+    per-call paths (one likelihood per MCMC step) skip the per-argument ctypes
+    object conversions (~1 us per call through byref / data_as)."""
+    proto = ctypes.CFUNCTYPE(_I, *([ctypes.c_void_p] * nargs))
+    return proto(ctypes.cast(getattr(_lib, name), ctypes.c_void_p).value)
+
+
+raw_wiener_like = _raw("wfpt_wiener_like", 5)
+raw_wiener_like_nodes = _raw("wfpt_wiener_like_nodes", 5)
 wfpt_pdf_array = _sig("wfpt_pdf_array", _I, [_VP, _PD, _I64, _PP, _PK, _I, _PD])
 wfpt_full_pdf = _sig("wfpt_full_pdf", _I, [_VP, _D, _PP, _PK, _PD])
 wfpt_wiener_like_multi = _sig("wfpt_wiener_like_multi", _I,

@@ -211,16 +211,28 @@ class Dataset:
         key = (err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         kc = getattr(self, "_kc", None)
         if kc is None or kc[0] != key:
-            kc = self._kc = (key, _lib.make_knobs(*key))
+            K = _lib.make_knobs(*key)
+            kc = self._kc = (key, K, ctypes.addressof(K))
         return kc[1]
+
+    def _knobs_addr(self, err, n_st, n_sz, use_adaptive, simps_err, w_outlier):
+        """The cached knobs struct's address (it lives in self._kc)."""
+        self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        return self._kc[2]
 
     def wiener_like(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10, use_adaptive=1,
                     simps_err=1e-8, p_outlier=0, w_outlier=0.1):
         P = _lib.make_params(v, sv, a, z, sz, t, st, p_outlier)
-        K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = ctypes.c_double()
-        _lib.check(_lib.wfpt_wiener_like(self.ctx.handle, self.handle, ctypes.byref(P),
-                                         ctypes.byref(K), ctypes.byref(out)))
+        c, h = self.ctx.handle, self.handle
+        if not c or not h:  # closed: the C ABI's own argument error
+            _lib.check(_lib.wfpt_wiener_like(c, h, ctypes.byref(P), ctypes.byref(self._kc[1]),
+                                             ctypes.byref(out)))
+        rc = _lib.raw_wiener_like(c.value, h.value, ctypes.addressof(P), kaddr,
+                                  ctypes.addressof(out))
+        if rc:
+            _lib.check(rc)
         return out.value
 
     def wiener_like_trials(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10, use_adaptive=1,
@@ -326,6 +338,22 @@ class Dataset:
         Returns the per-node summed log-likelihoods (float64[n_nodes]);
         trials=True: (per-node sums, per-trial log terms in the order the
         trials were given to the Dataset)."""
+        if not trials:
+            # the per-step MCMC call: plain addresses through the raw prototype
+            pm = np.ascontiguousarray(params, dtype=np.float64)
+            if self.n_nodes == 0:
+                raise ValueError("dataset was created without node ids")
+            if pm.shape != (self.n_nodes, 8):
+                raise ValueError(f"params must have shape ({self.n_nodes}, 8)")
+            kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+            out = np.empty(self.n_nodes, dtype=np.float64)
+            c, h = self.ctx.handle, self.handle
+            if c and h:
+                rc = _lib.raw_wiener_like_nodes(c.value, h.value, pm.ctypes.data, kaddr,
+                                                out.ctypes.data)
+                if rc:
+                    _lib.check(rc)
+                return out
         table, keep = self._node_table(params)
         K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = np.empty(self.n_nodes, dtype=np.float64)
