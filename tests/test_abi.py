@@ -130,3 +130,21 @@ def test_new_entry_points_reject_null_arguments_without_gpu():
     assert _lib.wfpt_wiener_like_nodes_local(None, None, None, None, None) == two
     assert _lib.wfpt_wiener_like_nodes_allreduce(None, None, None, 0, None, None) == two
     assert b"null" in _lib.wfpt_last_error()
+
+
+def test_raw_prototypes_bind_the_declared_entry_points():
+    """The binding's per-step fast path (raw-address prototypes) calls the
+    same C entry points as the declared ctypes functions, and a closed
+    dataset still gets the C ABI's argument error (no crash on a NULL)."""
+    from hddm_amd import _lib
+    for raw, decl in ((_lib.raw_wiener_like, _lib.wfpt_wiener_like),
+                      (_lib.raw_wiener_like_nodes, _lib.wfpt_wiener_like_nodes)):
+        assert (ctypes.cast(raw, ctypes.c_void_p).value ==
+                ctypes.cast(decl, ctypes.c_void_p).value)
+    # NULL context / dataset through the raw prototype: WFPT_ERR_ARG, no device
+    k = _lib.make_knobs(1e-4, 2, 2, 1, 1e-3, 0.1)
+    p = _lib.make_params(0.5, 0.1, 2.0, 0.5, 0.1, 0.3, 0.1, 0.05)
+    out = ctypes.c_double()
+    rc = _lib.raw_wiener_like(None, None, ctypes.addressof(p), ctypes.addressof(k),
+                              ctypes.addressof(out))
+    assert rc == 2
