@@ -135,10 +135,11 @@ def stress_line(ctx, steps, warmup, lib_path):
     per-call times, and the in-wave engine kernel (the level-0 pass these sets
     take) per launch from HIP events, with its executed-work fraction when
     profiles/traffic_stress.json was measured on this build."""
-    from hddm_amd import wfpt
+    from hddm_amd import _lib, wfpt
     kn = knobs_tuple()
-    call_s, k_ms, nl, evals, ntr = 0.0, 0.0, 0, 0, 0
-    for x, p in stress_sets():
+    call_s, evals, ntr = 0.0, 0, 0
+    sets = []
+    for si, (x, p) in enumerate(stress_sets()):
         ds = wfpt.Dataset(x)
         ctx.profile(ctx.PROF_EVALS)
         ds.wiener_like(*p, *kn)
@@ -153,7 +154,11 @@ def stress_line(ctx, steps, warmup, lib_path):
         for _ in range(steps):
             ds.wiener_like(*p, *kn)
         ctx.synchronize()
-        call_s += (time.perf_counter() - t0) / steps
+        el = (time.perf_counter() - t0) / steps
+        call_s += el
+        # the set's steady-state kernels: the engine (refining data) or the
+        # lean pass (a set whose waves settle at level 0)
+        engine = bool(ctx.last_path() & _lib.PATH_ENGINE)
         ctx.profile(ctx.PROF_EVENTS)
         ctx.profile_read(reset=True)
         for _ in range(steps):
@@ -161,25 +166,172 @@ def stress_line(ctx, steps, warmup, lib_path):
         ctx.synchronize()
         km, l, _ = ctx.profile_read(reset=True)
         ctx.profile(0)
-        k_ms += km / max(l, 1)
-        nl += 1
+        sets.append({"set": si, "call_ms": el * 1e3, "main_kernel": "engine" if engine else "lean",
+                     "main_kernel_ms": km / max(l, 1), "pdf_sv_evals_per_trial": ne / x.size})
         ds.close()
-    k_avg_s = k_ms / nl / 1e3
+    eng = [r for r in sets if r["main_kernel"] == "engine"]
+    k_avg_s = sum(r["main_kernel_ms"] for r in eng) / max(len(eng), 1) / 1e3
     out = {"workload": "4 x 250k full-DDM trials, parameters from hddm/generate.py:38-46 "
                        "ranges (seed 20261016), one resident wiener_like call per set",
            "trials_per_s": ntr / call_s, "ms_per_1M_trials": call_s * 1e3 * 1e6 / ntr,
-           "pdf_sv_evals_per_trial": evals / ntr,
-           "kernel": "wfpt::engine_kernel<3, false, 0> (in-wave adaptive engine)",
+           "pdf_sv_evals_per_trial": evals / ntr, "sets": sets,
+           "kernel": "wfpt::engine_kernel<3, false, 0> (in-wave adaptive engine), over the "
+                     "sets whose steady-state call runs it (%s)" % [r["set"] for r in eng],
            "kernel_ms_avg": k_avg_s * 1e3, "frac": None}
     pmc = pmc_summary(lib_path, "traffic_stress.json")
-    if pmc and pmc.get("matches_build"):
+    if pmc and pmc.get("matches_build") and eng:
+        # fp64 lane-ops per trial averaged over the engine launches of the same
+        # sets' steady-state calls (tools/stress_probe.py --engine-only under
+        # rocprofv3): equal launches per set, so n * mean(w) / mean(t) is the
+        # engine sets' total work over their total kernel time
         w = float(pmc["fp64_lane_ops_per_trial"])
         ach = STRESS_TRIALS * w / k_avg_s / 1e12
         tr = pmc.get("hbm_bytes_per_trial")
         out.update(achieved=ach, frac=ach / (PEAK_LANE_OPS / 1e12), fp64_lane_ops_per_trial=w,
                    valu_issue_utilisation=pmc.get("valu_issue_utilisation"),
                    traffic=tr * STRESS_TRIALS if tr is not None else None,
-                   algorithmic_bytes=8.0 * STRESS_TRIALS, pmc_source=pmc.get("source"))
+                   algorithmic_bytes=8.0 * STRESS_TRIALS, pmc_source=pmc.get("source"),
+                   pmc_sets=pmc.get("sets"))
+    return out
+
+
+C2_TRIALS = 10_000_000
+C2_PARAMS = (0.5, 0.0, 2.0, 0.5, 0.0, 0.3, 0.0)  # simple DDM (v, a, t), z = .5
+
+
+def c2_line(ctx, steps, warmup, lib_path):
+    """BASELINE config 2 under the same clock: the simple DDM (Navarro-Fuss
+    pdf, one pdf_sv per trial) over 10M resident trials, HDDM knobs,
+    p_outlier .05 (the same dataset as tools/c2_probe.py, seed 20261015); the
+    direct_kernel's per-launch time from HIP events and its executed-work
+    fraction when profiles/traffic_c2.json was measured on this build."""
+    from hddm_amd import wfpt
+    np.random.seed(20261015)
+    x = wfpt.gen_rts_from_cdf(*C2_PARAMS, samples=C2_TRIALS, dt=1e-3)
+    ds = wfpt.Dataset(x)
+    kn = knobs_tuple()
+    for _ in range(warmup):
+        v = ds.wiener_like(*C2_PARAMS, *kn)
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        v = ds.wiener_like(*C2_PARAMS, *kn)
+    ctx.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    ctx.profile(ctx.PROF_EVENTS)
+    ctx.profile_read(reset=True)
+    for _ in range(steps):
+        ds.wiener_like(*C2_PARAMS, *kn)
+    ctx.synchronize()
+    km, l, _ = ctx.profile_read(reset=True)
+    ctx.profile(0)
+    ds.close()
+    k_s = km / max(l, 1) / 1e3
+    out = {"workload": "C2: simple DDM (v=.5 a=2 z=.5 t=.3), 10M resident trials, one "
+                       "wiener_like call per step", "trials": C2_TRIALS,
+           "ms_per_step": el * 1e3, "trials_per_s": C2_TRIALS / el, "logp": v,
+           "kernel": "wfpt::direct_kernel<false>", "kernel_ms_avg": k_s * 1e3, "frac": None}
+    pmc = pmc_summary(lib_path, "traffic_c2.json")
+    if pmc and pmc.get("matches_build"):
+        w = float(pmc["fp64_lane_ops_per_trial"])
+        ach = C2_TRIALS * w / k_s / 1e12
+        tr = pmc.get("hbm_bytes_per_trial")
+        out.update(achieved=ach, frac=ach / (PEAK_LANE_OPS / 1e12), fp64_lane_ops_per_trial=w,
+                   valu_lane_ops_per_trial=pmc.get("valu_lane_ops_per_trial"),
+                   valu_issue_utilisation=pmc.get("valu_issue_utilisation"),
+                   traffic=tr * C2_TRIALS if tr is not None else None,
+                   algorithmic_bytes=8.0 * C2_TRIALS, pmc_source=pmc.get("source"))
+    return out
+
+
+C5_BLOCK = 12_500_000  # C5's 100M trials as 8 blocks (seed 20261015 + block)
+
+
+def c5_rts(lo, hi):
+    """Trials [lo, hi) of config 5's 100M: block b (12.5M trials) is sampled
+    with seed 20261015 + b, so every world size shards the same 100M trials
+    (rank r of N = 8 holds block r) and N = 1 holds all of them."""
+    parts = []
+    for b in range(lo // C5_BLOCK, (hi - 1) // C5_BLOCK + 1):
+        blk = make_rts(C5_BLOCK, 20261015 + b)
+        s, e = max(lo, b * C5_BLOCK), min(hi, (b + 1) * C5_BLOCK)
+        parts.append(blk[s - b * C5_BLOCK:e - b * C5_BLOCK])
+    return np.concatenate(parts)
+
+
+def c5_n1_line(ctx, steps, warmup):
+    """Config 5's whole workload on ONE GPU: the 100M trials every world size
+    shards (c5_rts), resident, through wiener_like_allreduce on a world-1 RCCL
+    communicator -- the N = 1 point of the 1/2/4/8-GPU curve on the same
+    workload and path as the N > 1 lines (value(N) / value_c5_n1 is the
+    speed-up)."""
+    from hddm_amd import dist as hdist
+    from hddm_amd import wfpt
+    t0 = time.perf_counter()
+    x = c5_rts(0, C5_TRIALS)
+    t_gen = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    ds = wfpt.Dataset(x)
+    t_ds = time.perf_counter() - t0
+    del x
+    hdist.init_comm(ctx, 0, 1)
+    step = lambda: ds.wiener_like_allreduce(*args_tuple(), *knobs_tuple())
+    for _ in range(warmup):
+        v = step()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        v = step()
+    ctx.synchronize()
+    el = (time.perf_counter() - t0) / steps
+    ds.close()
+    return {"workload": "C5 on 1 GPU: the same 100M full-DDM trials the N > 1 lines shard "
+                        "(12.5M blocks, seed 20261015 + block), one wiener_like_allreduce "
+                        "per step on a world-1 RCCL communicator",
+            "trials": C5_TRIALS, "ms_per_step": el * 1e3, "value": C5_TRIALS / el,
+            "unit": "trials/s", "logp": v, "data_generation_s": t_gen,
+            "dataset_create_s": t_ds}
+
+
+def c4_line(cpu_seconds=2.0):
+    """BASELINE config 4 under the same clock: HDDM(200 subjects x 500
+    trials, depends_on={'v': 'cond'}).sample(2000) on one GPU (after 20 burn-in
+    sweeps, hddm_amd.hierarchical), full DDM (sv, sz, st) and simple; beside
+    it the reference-port CPU likelihood time of one sweep's node evaluations
+    (oracle/wfpt_oracle.c wiener_like per 250-trial node, 1 thread, x the
+    sweep's node evaluations; the reference's PyMC sampler cannot run
+    offline)."""
+    import oracle
+    from hddm_amd.hierarchical import HDDM, gen_data
+    out = {"workload": "C4: HDDM 200 subj x 500 trials, depends_on v:cond, p_outlier .05, "
+                       "sample(2000) after 20 burn-in sweeps, data at dt 1e-4"}
+    for full in (True, False):
+        inter = dict(sv=0.1, sz=0.1, st=0.1) if full else {}
+        data, _ = gen_data(n_subj=200, n_trials=500, dt=1e-4, **inter)
+        m = HDDM(data, depends_on={"v": "cond"}, include=tuple(inter), p_outlier=0.05, seed=1)
+        m.sample(20)
+        c0, s0 = m.likelihood_calls, m.likelihood_seconds
+        t0 = time.perf_counter()
+        m.sample(2000)
+        el = time.perf_counter() - t0
+        calls = m.likelihood_calls - c0
+        node = data["rt"].to_numpy()[:250].copy()
+        p = (1.0, *((0.1,) if full else (0.0,)), 2.0, 0.5, *((0.1,) if full else (0.0,)), 0.3,
+             *((0.1,) if full else (0.0,)))
+        reps, t1 = 0, time.perf_counter()
+        while time.perf_counter() - t1 < cpu_seconds:
+            oracle.wiener_like(node, *p, 1e-4, 2, 2, 1, 1e-3, 0.05, 0.1)
+            reps += 1
+        per_node = (time.perf_counter() - t1) / reps
+        out["full" if full else "simple"] = {
+            "sample_2000_s": el, "sweeps_per_s": 2000 / el,
+            "batched_likelihood_calls_per_sweep": calls / 2000,
+            "likelihood_us_per_call": (m.likelihood_seconds - s0) / max(calls, 1) * 1e6,
+            "likelihood_fraction_of_time": (m.likelihood_seconds - s0) / el,
+            "cpu_port_likelihood_s_per_sweep": per_node * calls * m.n_nodes / 2000,
+            "cpu_port": {"kind": "port", "cores": 1, "per_node_call_s": per_node,
+                         "sample": f"{reps} wiener_like calls on one 250-trial node"}}
+        m.dataset.close()
     return out
 
 
@@ -229,6 +381,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stress", action="store_true",
                     help="skip the secondary stress-set figure (N = 1 only)")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the C2 and C5-on-one-GPU figures (N = 1 only)")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="skip the config-4 sample(2000) figures (N = 1 only)")
     a = ap.parse_args()
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -255,7 +411,10 @@ def main():
     else:
         lo, hi = _lib.shard_range(total, world, rank)
         n = hi - lo
-    x = make_rts(n, 20261015 + rank)
+    if c5 and a.trials is None:
+        x = c5_rts(lo, hi)  # the 100M trials' shard: the same data at every world size
+    else:
+        x = make_rts(n, 20261015 + rank)
     ds = wfpt.Dataset(x, device=local)
     if world > 1:
         from hddm_amd import dist as hdist
@@ -354,6 +513,14 @@ def main():
     }
     if world == 1 and not a.no_stress:
         out["stress"] = stress_line(ctx, a.steps, a.warmup, _lib.LIB_PATH)
+    if world == 1 and not a.no_extra:
+        ds.close()
+        out["c2"] = c2_line(ctx, a.steps, a.warmup, _lib.LIB_PATH)
+        out["c5_n1"] = c5_n1_line(ctx, a.steps, a.warmup)
+        out["config"]["c5_n1_speedup_basis"] = (
+            "value at N > 1 / c5_n1.value = the speed-up on config 5's one 100M workload")
+    if world == 1 and not a.no_c4:
+        out["c4"] = c4_line()
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(x, a.cpu_seconds)
     if rank == 0:

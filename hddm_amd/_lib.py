@@ -88,6 +88,13 @@ def _raw(name, nargs):
 
 raw_wiener_like = _raw("wfpt_wiener_like", 5)
 raw_wiener_like_nodes = _raw("wfpt_wiener_like_nodes", 5)
+wfpt_wiener_like_nodes_multi = _sig("wfpt_wiener_like_nodes_multi", _I,
+                                    [_VP, _VP, _PP, _I32, _PK, _PD])
+wfpt_wiener_like_nodes_multi_ex = _sig("wfpt_wiener_like_nodes_multi_ex", _I,
+                                       [_VP, _VP, _PP, _I32, _PK, _PD, _PD])
+_raw_multi_proto = ctypes.CFUNCTYPE(_I, _VP, _VP, _VP, _I32, _VP, _VP)
+raw_wiener_like_nodes_multi = _raw_multi_proto(
+    ctypes.cast(_lib.wfpt_wiener_like_nodes_multi, ctypes.c_void_p).value)
 wfpt_pdf_array = _sig("wfpt_pdf_array", _I, [_VP, _PD, _I64, _PP, _PK, _I, _PD])
 wfpt_full_pdf = _sig("wfpt_full_pdf", _I, [_VP, _D, _PP, _PK, _PD])
 wfpt_wiener_like_multi = _sig("wfpt_wiener_like_multi", _I,
@@ -147,6 +154,7 @@ EXPORTED = [
     "wfpt_wiener_like_nodes_ex", "wfpt_wiener_like_multi_ex", "wfpt_wiener_like_multi_resident_ex",
     "wfpt_wiener_like_trials", "wfpt_dataset_order", "wfpt_debug_partials", "wfpt_last_path",
     "wfpt_wiener_like_local", "wfpt_wiener_like_nodes_local", "wfpt_wiener_like_nodes_allreduce",
+    "wfpt_wiener_like_nodes_multi", "wfpt_wiener_like_nodes_multi_ex",
 ]
 
 # error encoding of a result triple (include/wfpt_amd.h: wfpt_decode_result)

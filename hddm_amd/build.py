@@ -94,5 +94,23 @@ def build(force=False, verbose=False, defines=(), out=None):
     return lib
 
 
+# Diagnostic builds that tests load in a child process (WFPT_AMD_LIB); never
+# the product. pubdiag: segment_publish_kernel's non-last blocks store their
+# sums after the completion word (tests/test_parity_trials.py:
+# test_stale_check_detects_late_publication).
+VARIANTS = {"pubdiag": ["WFPT_PUB_DIAG=1"]}
+
+
+def variant_path(name):
+    return os.path.join(LIBDIR, f"libwfpt_amd_{name}.so")
+
+
+def build_variants(force=False, verbose=False):
+    return [build(force=force, verbose=verbose, defines=d, out=variant_path(k))
+            for k, d in VARIANTS.items()]
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    if "--variants" in sys.argv:
+        print(build_variants(force="--force" in sys.argv, verbose=True))

@@ -230,6 +230,7 @@ struct wfpt_ds {
   // diagnostic calls are returned in the caller's order; kept in HBM, not in
   // host memory: 8 B per trial); null = identity (WFPT_DS_INPUT_ORDER)
   int64_t* perm = nullptr;
+  bool identity = true;  // stored order == the caller's order (perm never allocated)
 };
 
 namespace {
@@ -470,11 +471,13 @@ int finish_profile(wfpt_ctx* c) {
 // stale number.
 int wait_word(wfpt_ctx* c, const void* word) {
   if (c->spin) {
-    const volatile unsigned long long* w = reinterpret_cast<const volatile unsigned long long*>(word);
+    // the word is the device's system-scope release store (fin_write,
+    // segment_publish_kernel, publish_*): read it with acquire semantics, so
+    // every result store the device ordered before it is visible below
+    const unsigned long long* w = reinterpret_cast<const unsigned long long*>(word);
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned it = 1;; ++it) {
-      if (w[0] == c->seq) {
-        std::atomic_thread_fence(std::memory_order_acquire);
+      if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == c->seq) {
         if (c->profile) HIP_TRY(hipEventSynchronize(c->ev1));
         return WFPT_OK;
       }
@@ -482,7 +485,8 @@ int wait_word(wfpt_ctx* c, const void* word) {
         const hipError_t q = hipStreamQuery(c->stream);
         if (q != hipSuccess && q != hipErrorNotReady)
           return fail(WFPT_ERR_HIP, std::string("likelihood kernels: ") + hipGetErrorString(q));
-        if (q == hipSuccess && w[0] != c->seq) break;  // idle: let the stream sync decide
+        if (q == hipSuccess && __atomic_load_n(w, __ATOMIC_ACQUIRE) != c->seq)
+          break;  // idle: let the stream sync decide
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) break;
       }
     }
@@ -579,10 +583,52 @@ int run_sum_fast(wfpt_ctx* c, const wfpt_ds* d, const wfpt::Params& P, const wfp
 
 // |a| < |b| with NaN RTs last: a strict weak order for any input (the
 // dataset sorts must not hit std::stable_sort's undefined behaviour)
-bool abs_less_nan_last(double a, double b) {
-  const bool na = std::isnan(a), nb = std::isnan(b);
-  if (na || nb) return !na && nb;
-  return std::fabs(a) < std::fabs(b);
+// Stored order of a dataset: |rt| ascending with NaN RTs last (a strict weak
+// order for any input), as an unsigned key: |rt|'s bits (monotone for
+// non-negative doubles), every NaN one key above +inf. `upper_last` adds the boundary bit
+// (x > 0 sorts after x <= 0). Keys are equal exactly when neither comparator
+// orders the pair, so a stable sort by key is the stable comparator sort.
+uint64_t order_key(double r, bool upper_last) {
+  uint64_t b;
+  std::memcpy(&b, &r, sizeof(b));
+  b &= 0x7fffffffffffffffull;
+  if (std::isnan(r)) b = 0x7ff8000000000000ull;
+  return (upper_last && r > 0) ? (b | 0x8000000000000000ull) : b;
+}
+
+// Stable sort of idx by key[idx] (ties keep idx order): LSD radix, 16-bit
+// digits, for large datasets (C5's 100M trials: seconds instead of a minute
+// of comparator sorting); the comparator sort below 64k trials.
+void stable_order(std::vector<int64_t>& idx, const double* rt, bool upper_last) {
+  const size_t n = idx.size();
+  if (n < (1u << 16)) {
+    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
+      return order_key(rt[a], upper_last) < order_key(rt[b], upper_last);
+    });
+    return;
+  }
+  std::vector<uint64_t> k(n), k2(n);
+  std::vector<int64_t> i2(n);
+  for (size_t j = 0; j < n; ++j) k[j] = order_key(rt[idx[j]], upper_last);
+  std::vector<size_t> cnt(1u << 16);
+  for (int sh = 0; sh < 64; sh += 16) {
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (size_t j = 0; j < n; ++j) cnt[(k[j] >> sh) & 0xffffu]++;
+    if (cnt[(k[0] >> sh) & 0xffffu] == n) continue;  // one digit value: nothing moves
+    size_t acc = 0;
+    for (auto& c : cnt) {
+      const size_t t = c;
+      c = acc;
+      acc += t;
+    }
+    for (size_t j = 0; j < n; ++j) {
+      const size_t p = cnt[(k[j] >> sh) & 0xffffu]++;
+      k2[p] = k[j];
+      i2[p] = idx[j];
+    }
+    k.swap(k2);
+    idx.swap(i2);
+  }
 }
 
 // Per-trial values of a dataset's stored order (device) -> the caller's order
@@ -777,22 +823,19 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
     for (int64_t i = 0; i < n; ++i) cnt[node_id[i] + 1]++;
     for (int32_t j = 0; j < n_nodes; ++j) cnt[j + 1] += cnt[j];
     off = cnt;
+    // |rt| order first (stable), then a stable counting placement by node:
+    // grouped by node, |rt|-ordered inside a node, ties in input order
+    std::vector<int64_t> ord(n);
+    for (int64_t i = 0; i < n; ++i) ord[i] = i;
+    if (!keep_order) stable_order(ord, rt, false);
     std::vector<int64_t> pos(cnt.begin(), cnt.end() - 1);
-    for (int64_t i = 0; i < n; ++i) idx[pos[node_id[i]]++] = i;
-    if (!keep_order)
-      for (int32_t j = 0; j < n_nodes; ++j)
-        std::stable_sort(idx.begin() + off[j], idx.begin() + off[j + 1],
-                         [&](int64_t a, int64_t b) { return abs_less_nan_last(rt[a], rt[b]); });
+    for (int64_t q : ord) idx[pos[node_id[q]]++] = q;
   } else if (!keep_order) {
     // boundary first (x > 0 is the upper boundary, pdf.pxi:116), then |rt|:
     // the lean pass keeps a wave's root z grid in scalar registers when the
     // wave holds one boundary (wfpt_kernels.hip: lean_kernel)
     // (NaN RTs last in their group: a strict weak order for any input)
-    std::stable_sort(idx.begin(), idx.end(), [&](int64_t a, int64_t b) {
-      const bool ua = rt[a] > 0, ub = rt[b] > 0;
-      if (ua != ub) return ub;
-      return abs_less_nan_last(rt[a], rt[b]);
-    });
+    stable_order(idx, rt, true);
   }
   std::vector<double> hx(n);
   std::vector<int32_t> hn(node_id ? n : 0);
@@ -808,7 +851,8 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
   hipError_t e = hipMalloc((void**)&d->x, std::max<int64_t>(n, 1) * sizeof(double));
   if (e == hipSuccess && n > 0)
     e = hipMemcpy(d->x, hx.data(), n * sizeof(double), hipMemcpyHostToDevice);
-  if (e == hipSuccess && (!keep_order || node_id) && n > 0) {
+  d->identity = !((!keep_order || node_id) && n > 0);
+  if (e == hipSuccess && !d->identity) {
     e = hipMalloc((void**)&d->perm, n * sizeof(int64_t));
     if (e == hipSuccess) e = hipMemcpy(d->perm, idx.data(), n * sizeof(int64_t), hipMemcpyHostToDevice);
   }
@@ -938,13 +982,16 @@ int wfpt_wiener_like_trials(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* p,
 
 int wfpt_dataset_order(const wfpt_ds* d, int64_t* perm) {
   if (!d || (!perm && d->n > 0)) return fail(WFPT_ERR_ARG, "null pointer");
-  if (!d->ctx) return fail(WFPT_ERR_ARG, "the dataset's context was closed");
-  if (!d->perm) {
+  if (d->identity) {  // identity order (input-order or empty dataset): host only
     for (int64_t i = 0; i < d->n; ++i) perm[i] = i;
     return WFPT_OK;
   }
-  DeviceGuard g(d->ctx->device);
-  HIP_TRY(hipMemcpy(perm, d->perm, d->n * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (!d->ctx || !d->perm) return fail(WFPT_ERR_ARG, "the dataset's context was closed");
+  wfpt_ctx* c = d->ctx;
+  std::lock_guard<std::mutex> lk(c->mu);  // serialised with calls on the context
+  DeviceGuard g(c->device);
+  HIP_TRY(hipMemcpyAsync(perm, d->perm, d->n * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   return WFPT_OK;
 }
 
@@ -1034,30 +1081,34 @@ namespace {
 // selects, and the level-0 / chunk-engine / record kernels writing each
 // trial's term to c->lp.
 int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
-                 const wfpt::Knobs& K) {
+                 const wfpt::Knobs& K, int32_t n_tables = 1) {
   const int32_t m = d->n_nodes;
-  HIP_TRY(c->mnodep.reserve(m));
-  int mode = -2;  // the integration family every node selects, or -1 if mixed
-  for (int32_t j = 0; j < m; ++j) {
+  const int64_t T = std::max<int32_t>(n_tables, 1);
+  const int64_t rows = T * m;  // table t's node j at t m + j
+  HIP_TRY(c->mnodep.reserve(std::max<int64_t>(rows, 1)));
+  int mode = -2;  // the integration family every node of every table selects, or -1 if mixed
+  for (int64_t j = 0; j < rows; ++j) {
     c->mnodep.h[j] = to_params(&per_node[j]);
     const int mj = wfpt::select_mode(per_node[j].sz, per_node[j].st, K.use_adaptive);
     mode = (mode == -2 || mode == mj) ? mj : -1;
   }
   if (mode > wfpt::kAdaptTZ) mode = -1;  // fixed Simpson: generic kernel
   if (c->nodes_generic) mode = -1;
-  HIP_TRY(c->res.reserve((size_t)m + 1));
+  HIP_TRY(c->res.reserve((size_t)rows + 1));
   if (mode >= 0) {  // deferred records / listed chunks of the per-node fast path
-    HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(d->n, 1)));
-    HIP_TRY(c->nd_par.reserve(std::max<int64_t>(d->n, 1)));
-    HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>((d->n + 63) / 64, 1)));
+    HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(T * d->n, 1)));
+    HIP_TRY(c->nd_par.reserve(std::max<int64_t>(T * d->n, 1)));
+    HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>(T * ((d->n + 63) / 64), 1)));
   }
-  // the split level 0 (adaptive t families, non-counting calls): the call's
-  // node rows + root z grids in device memory
-  const bool split = (mode == wfpt::kAdaptT || mode == wfpt::kAdaptTZ) && !c->count && c->node_split;
-  const wfpt::NodeTables nt{m, split, !c->count && c->node_spec};
+  // the split level 0 (adaptive t families, non-counting one-table calls):
+  // the call's node rows + root z grids in device memory
+  const bool split = (mode == wfpt::kAdaptT || mode == wfpt::kAdaptTZ) && !c->count &&
+                     c->node_split && T == 1;
+  wfpt::NodeTables nt{m, split, !c->count && c->node_spec};
+  nt.n_tables = (int32_t)T;
   c->path = split ? WFPT_PATH_NODE_SPLIT : 0;
-  HIP_TRY(c->mnode.reserve((size_t)m + 2));
-  HIP_TRY(c->lp.reserve(std::max<int64_t>(d->n, 1)));
+  HIP_TRY(c->mnode.reserve((size_t)rows + 2));
+  HIP_TRY(c->lp.reserve(std::max<int64_t>(T * d->n, 1)));
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
   wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, mode, c->lp.p, c->nd_idx.p,
@@ -1117,6 +1168,47 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   return WFPT_OK;
 }
 
+int wfpt_wiener_like_nodes_multi_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* tables,
+                                    int32_t n_tables, const wfpt_knobs* k, double* out,
+                                    double* out_trial) {
+  if (int rc = nodes_check(c, d, tables, k, out)) return rc;
+  if (n_tables < 1) return fail(WFPT_ERR_ARG, "n_tables < 1");
+  const int32_t m = d->n_nodes;
+  if ((int64_t)n_tables * m > (int64_t)INT32_MAX / 2)
+    return fail(WFPT_ERR_ARG, "n_tables x n_nodes too large");
+  const wfpt::Knobs K = to_knobs(k);
+  WFPT_RANGE("wfpt_wiener_like_nodes_multi");
+  std::lock_guard<std::mutex> lk(c->mu);
+  DeviceGuard g(c->device);
+  const int32_t rows = n_tables * m;
+  if (int rc = nodes_launch(c, d, tables, K, n_tables)) return nodes_recover(c, rc);
+  ++c->seq;
+  if (rows > 0) {
+    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->mnode.d, c->status, c->seq,
+                             c->stream, c->ncnt + 3, c->ncnt, n_tables, d->n);
+    if (hipGetLastError() != hipSuccess)
+      return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_publish_kernel launch failed"));
+    if (int rc = wait_word(c, c->mnode.h + rows + 1)) return nodes_recover(c, rc);
+    if (int rc = check_status_value(c->mnode.h[rows])) return rc;
+  } else {
+    if (hipStreamSynchronize(c->stream) != hipSuccess)
+      return nodes_recover(c, fail(WFPT_ERR_HIP, "node pass failed on the device"));
+    (void)hipMemset(c->ncnt, 0, 4 * sizeof(int));
+  }
+  if (int rc = finish_profile(c)) return rc;
+  std::memcpy(out, c->mnode.h, (size_t)rows * sizeof(double));
+  if (out_trial)
+    for (int32_t t = 0; t < n_tables; ++t)
+      if (int rc = trials_to_caller(d, c->lp.p + (int64_t)t * d->n, out_trial + (int64_t)t * d->n))
+        return rc;
+  return WFPT_OK;
+}
+
+int wfpt_wiener_like_nodes_multi(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* tables,
+                                 int32_t n_tables, const wfpt_knobs* k, double* out) {
+  return wfpt_wiener_like_nodes_multi_ex(c, d, tables, n_tables, k, out, nullptr);
+}
+
 int wfpt_wiener_like_nodes_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
                                  const wfpt_knobs* k, double* out) {
   if (int rc = nodes_check(c, d, per_node, k, out)) return rc;
@@ -1126,11 +1218,15 @@ int wfpt_wiener_like_nodes_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_param
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
   if (int rc = nodes_launch(c, d, per_node, K)) return nodes_recover(c, rc);
+  // every exit after nodes_launch restores the node counters (0 at rest)
   wfpt::launch_segment_res(c->lp.p, d->off, m, c->res.p, c->status, false, c->stream, c->ncnt);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(out, c->res.p, ((size_t)m + 1) * sizeof(double), hipMemcpyDeviceToHost,
-                         c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (hipGetLastError() != hipSuccess)
+    return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_res launch failed"));
+  if (hipMemcpyAsync(out, c->res.p, ((size_t)m + 1) * sizeof(double), hipMemcpyDeviceToHost,
+                     c->stream) != hipSuccess)
+    return nodes_recover(c, fail(WFPT_ERR_HIP, "node vector copy failed"));
+  if (hipStreamSynchronize(c->stream) != hipSuccess)
+    return nodes_recover(c, fail(WFPT_ERR_HIP, "node pass failed on the device"));
   return finish_profile(c);
 }
 
@@ -1174,22 +1270,21 @@ int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_p
   if (hipGetLastError() != hipSuccess) {
     (void)ncclCommAbort(c->comm);
     c->comm = nullptr;
-    return fail(lrc != WFPT_OK ? lrc : WFPT_ERR_HIP,
-                lmsg + " (device stream unusable: RCCL communicator aborted)");
+    return nodes_recover(c, fail(lrc != WFPT_OK ? lrc : WFPT_ERR_HIP,
+                                 lmsg + " (device stream unusable: RCCL communicator aborted)"));
   }
   // per-node sums (and the error count) of every rank summed: a node's
   // -inf on any rank reaches every rank (wfpt.pyx:71-72 per node)
   const ncclResult_t nr = ncclAllReduce(c->res.p, c->res.p, (size_t)m + 1, ncclDouble, ncclSum,
                                         c->comm, c->stream);
-  if (lrc != WFPT_OK) {
-    (void)hipStreamSynchronize(c->stream);
-    return fail(lrc, lmsg);
-  }
+  if (lrc != WFPT_OK) return nodes_recover(c, fail(lrc, lmsg));
   if (nr != ncclSuccess)
-    return fail(WFPT_ERR_COMM, std::string("ncclAllReduce: ") + ncclGetErrorString(nr));
+    return nodes_recover(c, fail(WFPT_ERR_COMM, std::string("ncclAllReduce: ") +
+                                                    ncclGetErrorString(nr)));
   wfpt::launch_publish_vec(c->res.p, m, c->mnode.d, ++c->seq, c->stream);
-  HIP_TRY(hipGetLastError());
-  if (int rc = wait_word(c, c->mnode.h + m + 1)) return rc;
+  if (hipGetLastError() != hipSuccess)
+    return nodes_recover(c, fail(WFPT_ERR_HIP, "publish_vec_kernel launch failed"));
+  if (int rc = wait_word(c, c->mnode.h + m + 1)) return nodes_recover(c, rc);
   if (int rc = check_status_value(c->mnode.h[m])) return rc;
   if (int rc = finish_profile(c)) return rc;
   std::memcpy(out, c->mnode.h, m * sizeof(double));

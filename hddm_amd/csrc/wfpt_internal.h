@@ -131,9 +131,15 @@ void launch_poison(double* res, hipStream_t s);
 // node_split_kernel (five lanes per trial) instead of node_fast_kernel.
 // split: the adaptive t families take node_split_kernel; spec: the sparse
 // deferred trials take node_record_spec (non-counting calls)
+// n_tables: T parameter tables (P holds T x n_nodes rows, table t's node j at
+// t n_nodes + j) over the same trials in one launch; table t's terms land in
+// lp[t n, (t + 1) n), its deferred records carry virtual indices t n + i and
+// its listed chunks t ceil(n / 64) + c (d_idx / d_par up to T n records, clist
+// up to T ceil(n / 64) chunks).
 struct NodeTables {
   int32_t n_nodes;
   bool split, spec;
+  int32_t n_tables = 1;
 };
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
@@ -153,9 +159,11 @@ void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long
 // One launch (segment_publish_kernel): the per-node sums into res, then the
 // last block (ticket, 0 at rest) publishes them to out with the error word
 // and the completion word and resets counters[0..2] (0 at rest).
+// n_tables > 1: the T n_nodes sums of a multi-table call (table t's node j at
+// t n_nodes + j, its trials at t n + off[j] of lp; n = trials per table).
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s,
-                        int* ticket, int* counters);
+                        int* ticket, int* counters, int32_t n_tables = 1, int64_t n = 0);
 // wiener_like_multi with a uniform adaptive / direct family (mode): level-0
 // pass + deferred trials (d_idx / d_par hold up to n records, *n_defer must
 // be 0 on the stream) into lp[n], then per-block sums into part / zeros

@@ -1020,11 +1020,15 @@ __device__ inline void eng_tables_wave(const Params& P, EngTables& T, int lane) 
 // One wave per record, wave ids w0, w0 + nwaves, ...: the record's tables in
 // the wave's LDS, its level-0 t nodes as tasks, the refinement rounds, and on
 // lane 0 its density (tree17, the exact path or the per-lane walk) and term.
+// A record's index is virtual (t n_tab + i: trial i of parameter table t, the
+// multi-table node call); its RT is x[i], its term lp[t n_tab + i].
+__device__ inline int64_t tab_trial(int64_t v, int64_t n_tab) { return v < n_tab ? v : v % n_tab; }
 template <int MODE, bool COUNT, bool MULTI>
 __device__ inline void node_records(ChunkLds<1>& cl, int lane, int w0, int nwaves,
                                     const double* x, const Knobs& K, double* lp,
                                     const int64_t* d_idx, const Params* d_par, int nd,
-                                    unsigned long long* evals, int* status) {
+                                    unsigned long long* evals, int* status,
+                                    int64_t n_tab = INT64_MAX) {
   long long ne = 0;
   int errf = 0;
   for (int k = w0; k < nd; k += nwaves) {
@@ -1035,7 +1039,7 @@ __device__ inline void node_records(ChunkLds<1>& cl, int lane, int w0, int nwave
     A.P = Q;
     A.K = K;
     A.wp_outlier = K.w_outlier * Q.p_outlier;
-    const double x0 = x[i];
+    const double x0 = x[tab_trial(i, n_tab)];
     eng_tables_wave(Q, cl.tab, lane);
     cl.X[lane] = lane == 0 ? x0 : 0.0;
     cl.fl[lane] = (lane == 0 && trial_setup(x0, Q).valid) ? 0 : (int)kFlagIdle;
@@ -1172,6 +1176,13 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void trial_kernel(TrialArg
 // pinned host memory. Resets the device status word. Fixed summation order
 // for a given nb: thread k owns partials k + 1024 j, loaded kFinLoads at a
 // time (all in flight together) and summed in j order; then a fixed tree.
+// The completion word of a result slot in mapped host memory: a system-scope
+// release store, after every result store the call's publication ordered
+// before it; the host reads it with an acquire load (wait_word).
+__device__ __forceinline__ void publish_word(unsigned long long* w, unsigned long long seq) {
+  __hip_atomic_store(w, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The result slot of a call (finalize's last step, one thread): {sum, zero
 // count, encoded errors, flags, -, heavy chunks, #tree} and then the
 // completion word; resets the device status word.
@@ -1203,11 +1214,10 @@ __device__ inline void fin_write(double t, long long zz, int dd, int* status, do
     mirror[5] = out[5];
     mirror[6] = out[6];
   }
-  __threadfence_system();
-  // completion word, written after the results are visible: the host may
-  // poll it instead of waiting on the stream
-  reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
-  __threadfence_system();
+  // completion word, a system-scope release store after the results (one
+  // thread wrote them all): the host may poll it (acquire) instead of waiting
+  // on the stream
+  publish_word(reinterpret_cast<unsigned long long*>(out) + 4, seq);
 }
 
 // Large nb (C2's 10M trials: 156k partials): one block is bound by a single
@@ -1588,9 +1598,7 @@ __global__ __launch_bounds__(64) void publish_kernel(const double* res, double* 
     out[3] = res[3];
     out[5] = res[5];
     out[6] = res[6];
-    __threadfence_system();
-    reinterpret_cast<volatile unsigned long long*>(out)[4] = seq;
-    __threadfence_system();
+    publish_word(reinterpret_cast<unsigned long long*>(out) + 4, seq);
   }
 }
 
@@ -1633,45 +1641,60 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
                                                             int* status, double* out,
                                                             unsigned long long seq) {
   for (int j = threadIdx.x; j < n; j += 256) out[j] = res[j];
-  __threadfence_system();
-  __syncthreads();
+  __syncthreads();  // every thread's stores happen-before thread 0's release
   if (threadIdx.x == 0) {
     const int st = atomicExch(status, 0);
     out[n] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
-    __threadfence_system();
-    reinterpret_cast<volatile unsigned long long*>(out + n + 1)[0] = seq;
-    __threadfence_system();
+    publish_word(reinterpret_cast<unsigned long long*>(out + n + 1), seq);
   }
 }
 
 // segment_sum_kernel's per-node sums and publish_nodes_kernel's publication in
-// one launch: each node's wave writes its sum to the device vector res, its
-// block releases them and adds to an agent-scope ticket; the last block
-// copies the sums to the mapped slot, writes the encoded error flags and,
-// after a system fence, the completion word, and resets the call's counters
-// (r05: the waves' direct writes to the mapped slot, ordered only by their
-// own completion, once let the completion word overtake a node's sum; the
-// node path's
-// n_defer words and the ticket: 0 at rest, stream order).
-#ifndef WFPT_PUB_WT
-#define WFPT_PUB_WT 1
+// one launch. The ordering is the memory model's, not the hardware's (LLVM
+// AMDGPUUsage memory model for GFX942/GFX950, the HSA / OpenCL 2.0 scoped
+// model: happens-before is the transitive closure of program order and scoped
+// synchronizes-with edges, each edge between threads inside its scope):
+//   1. lane 0 of node j's wave stores res[j] (device memory; an agent-scope
+//      atomic store, performed at agent scope before the wave goes on);
+//   2. __syncthreads (workgroup-scope release + acquire): every store of the
+//      block happens-before thread 0's next operation;
+//   3. thread 0: acq_rel fetch_add on the agent-scope ticket. The ticket's
+//      RMWs form one release sequence, so the block that draws G - 1
+//      synchronizes-with every earlier block's release;
+//   4. __syncthreads: the last block's threads happen-after all G releases,
+//      read res[] and store it to the mapped slot;
+//   5. __syncthreads, then thread 0 stores the completion word with a
+//      system-scope release; the host polls it with an acquire load
+//      (wfpt_capi.cpp: wait_word), so every sum is visible when it reads.
+// r05 let each wave store its sum straight into the mapped slot, ordered
+// before the completion word by nothing: one GPU-suite run read a node sum
+// of the previous call (profiles/r06/stale_diag/ shows the test catching that
+// order deterministically in the WFPT_PUB_DIAG build). The last block also
+// resets the call's counters (the node path's n_defer words and the ticket:
+// 0 at rest, stream order).
+//
+// WFPT_PUB_DIAG=1 (diagnostic builds only, never the shipped library): every
+// block but the last takes its ticket *first* and writes its nodes' sums into
+// the mapped slot ~70 us later, i.e. the completion word deterministically
+// overtakes the sums -- the failure the regression test must be able to see.
+#ifndef WFPT_PUB_DIAG
+#define WFPT_PUB_DIAG 0
 #endif
-// WFPT_PUB_DIRECT=1 (diagnostic builds only): each wave writes its node's sum
-// straight to the mapped slot, as r05 first did (test_node_sums_never_stale
-// is the check that catches it)
-#ifndef WFPT_PUB_DIRECT
-#define WFPT_PUB_DIRECT 0
-#endif
+// Multi-table calls: n_nodes = T m virtual nodes, node j of table t at
+// t m + j, summing trials [t n + off[j], t n + off[j + 1]) of lp.
 __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, const int64_t* off,
                                                               int32_t n_nodes, int* status,
                                                               double* res, double* out,
                                                               unsigned long long seq, int* ticket,
-                                                              int* counters) {
+                                                              int* counters, int32_t m_tab,
+                                                              int64_t n_tab) {
   __shared__ int last;
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  double sum = 0.0;
   if (j < n_nodes) {
-    const int64_t lo = off[j], hi = off[j + 1];
+    const int tab = j / m_tab, jr = j - tab * m_tab;
+    const int64_t lo = tab * n_tab + off[jr], hi = tab * n_tab + off[jr + 1];
     double s = 0.0;
     int zero = 0;
     for (int64_t i = lo + lane; i < hi; i += 64) {
@@ -1681,36 +1704,33 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
     }
     s = wave_sum(s);
     const bool anyz = __ballot(zero != 0) != 0ull;
-    if (lane == 0) {
-#if WFPT_PUB_DIRECT
-      out[j] = anyz ? -INFINITY : s;  // (diagnostic: the racy r05 form, tests only)
-#elif WFPT_PUB_WT
-      __hip_atomic_store(&res[j], anyz ? -INFINITY : s, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-#else
-      res[j] = anyz ? -INFINITY : s;
-#endif
+    sum = anyz ? -INFINITY : s;
+    if (!WFPT_PUB_DIAG && lane == 0) {  // (1)
+      __hip_atomic_store(&res[j], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // the storing wave waits for its agent-scope store to be performed:
+      // LLVM's workgroup barrier does not wait for other waves' vector
+      // stores (non-tgsplit gfx950 emits only lgkmcnt(0) before s_barrier),
+      // and thread 0's release below waits only for its own wave's
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
-  // device-memory sums made visible at agent scope before the block's ticket
-  // (WFPT_PUB_WT: agent-coherent stores, waited for; else finalize_kernel's
-  // release fence); the last block alone writes the mapped slot, so one
-  // thread order + one system fence precede the completion word
-#if WFPT_PUB_WT
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
-  __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+  __syncthreads();  // (2)
+  if (threadIdx.x == 0)  // (3)
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
            (int)gridDim.x - 1;
-  __syncthreads();
+  __syncthreads();  // (4)
+#if WFPT_PUB_DIAG
+  if (!last) {
+    for (int r = 0; r < 20; ++r) __builtin_amdgcn_s_sleep(127);
+    if (j < n_nodes && lane == 0) out[j] = sum;  // after the word: stale reads follow
+    return;
+  }
+  if (j < n_nodes && lane == 0) out[j] = sum;
+#else
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  if (!WFPT_PUB_DIRECT)
-    for (int k = threadIdx.x; k < n_nodes; k += 256)
-      out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = threadIdx.x; k < n_nodes; k += 256)
+    out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   if (threadIdx.x == 0) {
     *ticket = 0;
     counters[0] = 0;
@@ -1719,12 +1739,9 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
     const int st = atomicExch(status, 0);
     out[n_nodes] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
   }
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    reinterpret_cast<volatile unsigned long long*>(out + n_nodes + 1)[0] = seq;
-    __threadfence_system();
-  }
+  __syncthreads();  // (5)
+  if (threadIdx.x == 0)
+    publish_word(reinterpret_cast<unsigned long long*>(out + n_nodes + 1), seq);
 }
 
 // Node all-reduce (wfpt_wiener_like_nodes_allreduce): the encoded error
@@ -1749,12 +1766,8 @@ __global__ __launch_bounds__(256) void node_poison_kernel(double* res, int32_t n
 __global__ __launch_bounds__(256) void publish_vec_kernel(const double* res, int32_t n,
                                                           double* out, unsigned long long seq) {
   for (int j = threadIdx.x; j <= n; j += 256) out[j] = res[j];
-  __threadfence_system();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    reinterpret_cast<volatile unsigned long long*>(out + n + 1)[0] = seq;
-    __threadfence_system();
-  }
+  __syncthreads();  // every thread's stores happen-before thread 0's release
+  if (threadIdx.x == 0) publish_word(reinterpret_cast<unsigned long long*>(out + n + 1), seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1829,11 +1842,19 @@ template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
                       double* lp, int64_t* d_idx, Params* d_par, int* n_defer, int* clist,
-                      int* n_chunks, unsigned long long* evals, int* status, int* prof) {
+                      int* n_chunks, unsigned long long* evals, int* status, int* prof,
+                      int32_t n_nodes, int64_t nw_tab) {
 #ifdef WFPT_NODE_DEBUG_FAST
   const long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
   exp_table_init();
+  // parameter table blockIdx.y (multi-table calls: T tables x the same
+  // trials): its rows, its terms lp[t n + i], its records' virtual indices
+  // t n + i and its chunks' ids t nw_tab + c
+  const int64_t tab = blockIdx.y;
+  P += tab * n_nodes;
+  lp += tab * n;
+  const int64_t vbase = tab * n, cbase = tab * nw_tab;
   __shared__ Params rows[kStageRows];
   __shared__ RootGrids grids[kNodeGridRows];
   const int64_t i0 = (int64_t)blockIdx.x * kBlock;
@@ -1902,13 +1923,13 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
       // node_engine_kernel (fast-pass records counted in n_chunks[2])
       int base = 0;
       if (lane == 0) {
-        clist[atomicAdd(n_chunks, 1)] = (int)(i >> 6);
+        clist[atomicAdd(n_chunks, 1)] = (int)(cbase + (i >> 6));
         base = atomicAdd(n_chunks + 2, __popcll(b));
       }
       base = __shfl(base, 0, 64);
       if (defer) {
         const int k = base + __popcll(b & lanemask_lt(lane));
-        d_idx[k] = i;
+        d_idx[k] = vbase + i;
         d_par[k] = Q;
       }
     }
@@ -2269,7 +2290,8 @@ template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
-    unsigned long long* evals, int* status, int* prof, int spec) {
+    unsigned long long* evals, int* status, int* prof, int spec, int32_t n_nodes,
+    int64_t nw_tab) {
 #ifdef WFPT_NODE_DEBUG
   const long long dbg_entry = __builtin_amdgcn_s_memrealtime();
 #else
@@ -2291,27 +2313,37 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
           // one block per record, its waves side by side (wave 0's LDS)
           ChunkLds<1>& c0 = lds[0];
           const int wv = threadIdx.x >> 6;
-          for (int k = (int)blockIdx.x; k < nrec; k += (int)gridDim.x)
-            node_record_spec<MODE, kEngWaves>(c0.F, c0.X, c0.fl, c0.tab, wv, lane, x, K, lp,
-                                              r_idx[k], r_par[k], errf, dbg_entry);
+          for (int k = (int)blockIdx.x; k < nrec; k += (int)gridDim.x) {
+            const int64_t v = r_idx[k];  // virtual: table t's trial i at t n + i
+            node_record_spec<MODE, kEngWaves>(c0.F, c0.X, c0.fl, c0.tab, wv, lane,
+                                              x + tab_trial(v, n), K, lp + v, 0, r_par[k], errf,
+                                              dbg_entry);
+          }
         } else {
-          for (int k = w0; k < nrec; k += nwaves)
-            node_record_spec<MODE, 1>(cl.F, cl.X, cl.fl, cl.tab, 0, lane, x, K, lp, r_idx[k],
-                                      r_par[k], errf, dbg_entry);  // F: 1088 doubles, fl: 64 ints
+          for (int k = w0; k < nrec; k += nwaves) {
+            const int64_t v = r_idx[k];
+            node_record_spec<MODE, 1>(cl.F, cl.X, cl.fl, cl.tab, 0, lane, x + tab_trial(v, n), K,
+                                      lp + v, 0, r_par[k], errf,
+                                      dbg_entry);  // F: 1088 doubles, fl: 64 ints
+          }
         }
         if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
         return;
       }
     }
     node_records<MODE, COUNT, false>(cl, lane, w0, nwaves, x, K, lp, r_idx, r_par, nrec, evals,
-                                     status);
+                                     status, n);
     return;
   }
   long long ne = 0;
   int nseg = 0, nex = 0, nwk = 0, errf = 0;
   Tally ty;
   for (int k = w0; k < nc; k += nwaves) {
-    const int64_t c = clist[k];
+    const int64_t vc = clist[k];  // virtual: table t's chunk c at t nw_tab + c
+    const int64_t tab = vc / nw_tab;
+    const int64_t c = vc - tab * nw_tab;
+    const Params* Pt = P + tab * n_nodes;
+    double* lpt = lp + tab * n;
     const int64_t i = c * 64 + lane;
     const bool own = i < n;
     const double x0 = own ? x[i] : 0.0;
@@ -2323,7 +2355,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
       const bool mine = todo && nj == jn;
       todo = todo && !mine;
       ++nseg;
-      const Params Q = P[__builtin_amdgcn_readfirstlane(jn)];
+      const Params Q = Pt[__builtin_amdgcn_readfirstlane(jn)];
       TrialArgs A{};
       A.x = x;
       A.n = n;
@@ -2382,7 +2414,7 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
       }
       if (mine) {
         if (oc != kFinal) ne += n1;  // node_fast_kernel counted the trials it settled
-        lp[i] = node_logp(p, Q, K);
+        lpt[i] = node_logp(p, Q, K);
       }
       wave_sync();  // the next segment rebuilds this wave's LDS
     }
@@ -2765,9 +2797,12 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
                                   unsigned long long* evals, int* status, int* prof,
                                   hipStream_t s, const NodeTables* nt) {
   bool split = false, spec = false;
+  const int T = nt ? std::max(nt->n_tables, 1) : 1;
+  const int32_t m = nt ? nt->n_nodes : 0;
+  const int64_t nw = (n + 63) / 64;
   if constexpr ((MODE == kAdaptT || MODE == kAdaptTZ) && !COUNT) {
     spec = nt && nt->spec;
-    if (nt && nt->split && nt->n_nodes > 0) {
+    if (nt && nt->split && nt->n_nodes > 0 && T == 1) {
       // the call's node tables, then the t-node split level 0; the chunk
       // engine / records below read the device copy of the rows
       hipLaunchKernelGGL((node_split_kernel<MODE>), dim3((n + 63) / 64), dim3(kNodeSplit * 64), 0,
@@ -2776,18 +2811,17 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     }
   }
   if (!split)
-    hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n)), dim3(kBlock), 0, s, x,
-                       node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
-                       prof);
+    hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n), T), dim3(kBlock), 0, s,
+                       x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
+                       prof, m, nw);
   if constexpr (MODE != kDirect) {
     // adaptive families, one launch: the fast pass's records one wave each
     // when they are sparse in their chunks, else one wave per listed chunk
     // (node_chunk_kernel reads the counts and picks)
-    const int64_t nw = (n + 63) / 64;
-    const int64_t nb = std::min<int64_t>((nw + kEngWaves - 1) / kEngWaves, 2048);
+    const int64_t nb = std::min<int64_t>((T * nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
                        n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof,
-                       spec ? 1 : 0);
+                       spec ? 1 : 0, m, nw);
   }
   // direct family: node_fast_kernel settles its exact-path trials itself
 }
@@ -2826,19 +2860,25 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
     return;
   }
   const int stk = stack_kind(K);
-#define NODE_LAUNCH(S_, C_)                                                                  \
-  hipLaunchKernelGGL((node_kernel<S_, C_>), dim3(nb), dim3(kBlock), 0, s, x, node, n, P, K, \
-                     lp, evals, status)
-  if (evals) {
-    if (stk == 0) NODE_LAUNCH(0, true);
-    else if (stk == 1) NODE_LAUNCH(1, true);
-    else NODE_LAUNCH(2, true);
-  } else {
-    if (stk == 0) NODE_LAUNCH(0, false);
-    else if (stk == 1) NODE_LAUNCH(1, false);
-    else NODE_LAUNCH(2, false);
-  }
+  // mixed families: the generic per-trial kernel once per parameter table
+  const int T = nt ? std::max(nt->n_tables, 1) : 1;
+  for (int t = 0; t < T; ++t) {
+    const Params* Pt = P + (int64_t)t * (nt ? nt->n_nodes : 0);
+    double* lpt = lp + (int64_t)t * n;
+#define NODE_LAUNCH(S_, C_)                                                                     \
+  hipLaunchKernelGGL((node_kernel<S_, C_>), dim3(nb), dim3(kBlock), 0, s, x, node, n, Pt, K, \
+                     lpt, evals, status)
+    if (evals) {
+      if (stk == 0) NODE_LAUNCH(0, true);
+      else if (stk == 1) NODE_LAUNCH(1, true);
+      else NODE_LAUNCH(2, true);
+    } else {
+      if (stk == 0) NODE_LAUNCH(0, false);
+      else if (stk == 1) NODE_LAUNCH(1, false);
+      else NODE_LAUNCH(2, false);
+    }
 #undef NODE_LAUNCH
+  }
 }
 
 void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
@@ -2861,10 +2901,11 @@ void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long
 
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s,
-                        int* ticket, int* counters) {
+                        int* ticket, int* counters, int32_t n_tables, int64_t n) {
   if (n_nodes <= 0) return;
-  hipLaunchKernelGGL(segment_publish_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                     n_nodes, status, res, out, seq, ticket, counters);
+  const int32_t nv = n_nodes * std::max(n_tables, 1);  // virtual nodes t m + j
+  hipLaunchKernelGGL(segment_publish_kernel, dim3((nv + 3) / 4), dim3(256), 0, s, lp, off, nv,
+                     status, res, out, seq, ticket, counters, n_nodes, n);
 }
 
 template <int MODE, bool COUNT>

@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -144,6 +145,26 @@ bool connect_by(int fd, const sockaddr_storage& sa, socklen_t len, Clock::time_p
   }
 }
 
+// The address is a loopback one (127/8 or ::1, incl. v4-mapped).
+bool is_loopback(const sockaddr_storage& sa) {
+  if (sa.ss_family == AF_INET) {
+    const uint32_t a = ntohl(reinterpret_cast<const sockaddr_in*>(&sa)->sin_addr.s_addr);
+    return (a >> 24) == 127u;
+  }
+  if (sa.ss_family == AF_INET6) {
+    const in6_addr& a = reinterpret_cast<const sockaddr_in6*>(&sa)->sin6_addr;
+    if (IN6_IS_ADDR_LOOPBACK(&a)) return true;
+    return IN6_IS_ADDR_V4MAPPED(&a) && a.s6_addr[12] == 127;
+  }
+  return false;
+}
+
+// `host` names loopback literally (a single-node job that asked for it).
+bool literal_loopback(const char* host) {
+  return std::strcmp(host, "localhost") == 0 || std::strncmp(host, "127.", 4) == 0 ||
+         std::strcmp(host, "::1") == 0;
+}
+
 }  // namespace
 
 extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int port,
@@ -160,6 +181,15 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
     sockaddr_storage la = sa;
     socklen_t llen = slen;
     if (bind_any()) llen = wildcard(sa.ss_family, port, &la);
+    // a host name that resolves to a loopback alias (127.0.1.1 from
+    // /etc/hosts) makes rank 0 unreachable for peers on other nodes: say so
+    // now, and again in the timeout error, rather than fail silently
+    const bool lo_alias = !bind_any() && is_loopback(la) && !literal_loopback(host);
+    if (lo_alias)
+      std::fprintf(stderr,
+                   "wfpt rendezvous: rank 0 listens on a loopback address (%s resolves to one); "
+                   "peers on other nodes cannot connect: set WFPT_COMM_BIND=any\n",
+                   host);
     Fd ls;
     ls.fd = ::socket(la.ss_family, SOCK_STREAM, 0);
     if (ls.fd < 0) return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: socket() failed");
@@ -177,7 +207,13 @@ extern "C" int wfpt_comm_exchange_id(int nranks, int rank, const char* host, int
       if (pr <= 0)
         return wfpt_rdv_fail(WFPT_ERR_COMM, "rendezvous: timed out with " + std::to_string(got) +
                                                 " of " + std::to_string(nranks - 1) +
-                                                " peers served");
+                                                " peers served" +
+                                                (lo_alias ? std::string(" (rank 0 listened on the "
+                                                                        "loopback address ") +
+                                                                host +
+                                                                " resolves to; remote peers need "
+                                                                "WFPT_COMM_BIND=any)"
+                                                          : std::string()));
       Fd c;
       c.fd = ::accept(ls.fd, nullptr, nullptr);
       if (c.fd < 0) continue;

@@ -82,13 +82,21 @@ def beta_logpdf(x, a, b):
 
 # ---------------------------------------------------------------- slice sampler
 
-def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200):
+def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_pair=None):
     """Vectorised univariate slice sampling (stepping out + shrinkage).
 
     x0: (n,) current values of n conditionally independent coordinates;
     logp(x) -> (n,) log conditional of each coordinate evaluated at x (one
     batched likelihood call). Returns the new values and the number of logp
     calls used.
+
+    logp_pair(xl, xr) -> (f(xl), f(xr)) (optional: both probes in ONE batched
+    call, wfpt_wiener_like_nodes_multi with two tables): the left and right
+    stepping-out run side by side. Given y and the initial interval the two
+    sides are independent (Neal 2003, fig. 3), so L, R -- and with the same
+    random numbers the whole step -- are those of the side-by-side-free loop;
+    only the number of calls drops (max of the two sides' steps instead of
+    their sum).
     """
     x0 = np.asarray(x0, dtype=np.float64)
     n = x0.size
@@ -98,23 +106,55 @@ def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200):
     R = L + w
     if lower is not None:
         L = np.maximum(L, lower)
-    for side in (0, 1):
-        active = np.ones(n, dtype=bool)
-        for _ in range(max_steps):
-            probe = np.where(active, L if side == 0 else R, x0)
-            f = logp(probe)
-            calls += 1
-            grow = active & (f > y)
-            if not grow.any():
-                break
-            if side == 0:
-                L = np.where(grow, L - w, L)
-                if lower is not None:
-                    L = np.maximum(L, lower)
-                    grow &= L > lower
+
+    def grow_left(active, f):
+        nonlocal L
+        grow = active & (f > y)
+        L = np.where(grow, L - w, L)
+        if lower is not None:
+            L = np.maximum(L, lower)
+            grow &= L > lower
+        return grow
+
+    def grow_right(active, f):
+        nonlocal R
+        grow = active & (f > y)
+        R = np.where(grow, R + w, R)
+        return grow
+
+    if logp_pair is not None:
+        act_l = np.ones(n, dtype=bool)
+        act_r = np.ones(n, dtype=bool)
+        steps_l = steps_r = 0
+        while True:
+            do_l = steps_l < max_steps and act_l.any()
+            do_r = steps_r < max_steps and act_r.any()
+            if do_l and do_r:
+                fl, fr = logp_pair(np.where(act_l, L, x0), np.where(act_r, R, x0))
+            elif do_l:
+                fl = logp(np.where(act_l, L, x0))
+            elif do_r:
+                fr = logp(np.where(act_r, R, x0))
             else:
-                R = np.where(grow, R + w, R)
-            active = grow
+                break
+            calls += 1
+            if do_l:
+                act_l = grow_left(act_l, fl)
+                steps_l += 1
+            if do_r:
+                act_r = grow_right(act_r, fr)
+                steps_r += 1
+    else:
+        for side in (0, 1):
+            active = np.ones(n, dtype=bool)
+            for _ in range(max_steps):
+                probe = np.where(active, L if side == 0 else R, x0)
+                f = logp(probe)
+                calls += 1
+                grow = grow_left(active, f) if side == 0 else grow_right(active, f)
+                if not grow.any():
+                    break
+                active = grow
     x1 = x0.copy()
     done = np.zeros(n, dtype=bool)
     for _ in range(max_shrink):
@@ -145,8 +185,11 @@ class HDDM:
     FAMILIES = ("a", "v", "t")
 
     def __init__(self, data, depends_on=None, include=(), p_outlier=0.05, wiener_params=None,
-                 seed=None, device=None):
+                 seed=None, device=None, paired_probes=True):
         import pandas as pd
+        # both stepping-out probes of a slice step in one two-table call
+        # (slice_step's logp_pair): the same chain, fewer likelihood calls
+        self.paired_probes = bool(paired_probes)
         self.data = data = pd.DataFrame(data).reset_index(drop=True)
         self.depends = {k: ([v] if isinstance(v, str) else list(v))
                         for k, v in (depends_on or {}).items()}
@@ -249,6 +292,22 @@ class HDDM:
         st[1] += dt
         return out
 
+    def node_logp_multi(self, overs):
+        """node_logp for several overrides in ONE launch (list of `over` dicts
+        -> (len(overs), n_nodes)): wfpt_wiener_like_nodes_multi, each row bit
+        for bit the one-table call's."""
+        t0 = time.perf_counter()
+        out = self.dataset.wiener_like_nodes_multi(np.stack([self.node_table(o) for o in overs]),
+                                                   **self.wp)
+        dt = time.perf_counter() - t0
+        self.likelihood_seconds += dt
+        self.likelihood_calls += 1
+        key = ",".join(sorted(overs[0])) + f" x{len(overs)}"
+        st = self.call_stats.setdefault(key, [0, 0.0])
+        st[0] += 1
+        st[1] += dt
+        return out
+
     def _unit_group(self, fam):
         """Group mean of each unit of `fam` (a float when the family has one
         level: the scalar fast path of the prior densities)."""
@@ -287,9 +346,15 @@ class HDDM:
             ll = np.bincount(unit, weights=self.node_logp({fam: x}), minlength=nu)
             return ll + self.subj_prior(fam, x)
 
+        def logp_pair(xl, xr):
+            r = self.node_logp_multi([{fam: xl}, {fam: xr}])
+            return (np.bincount(unit, weights=r[0], minlength=nu) + self.subj_prior(fam, xl),
+                    np.bincount(unit, weights=r[1], minlength=nu) + self.subj_prior(fam, xr))
+
         lower = 0.0 if fam in ("a", "t") else None
         self.subj[fam], _ = slice_step(self.subj[fam], logp, SLICE_WIDTHS[fam], self.rng,
-                                       lower=lower)
+                                       lower=lower,
+                                       logp_pair=logp_pair if self.paired_probes else None)
 
     def _update_group(self, fam):
         nl = len(self.levels[fam])
@@ -337,8 +402,18 @@ class HDDM:
                 return np.array([-np.inf])
             return np.array([pr + float(np.sum(self.node_logp({name: val})))])
 
+        def logp_pair(xl, xr):
+            vals = (float(xl[0]), float(xr[0]))
+            prs = [float(prior(v)) for v in vals]
+            live = [v for v, pr in zip(vals, prs) if np.isfinite(pr)]
+            if len(live) < 2:  # a probe outside the prior's support: no likelihood needed
+                return logp(xl), logp(xr)
+            r = self.node_logp_multi([{name: vals[0]}, {name: vals[1]}])
+            return (np.array([prs[0] + float(np.sum(r[0]))]),
+                    np.array([prs[1] + float(np.sum(r[1]))]))
+
         new, _ = slice_step(np.array([self.inter[name]]), logp, SLICE_WIDTHS[name], self.rng,
-                            lower=0.0)
+                            lower=0.0, logp_pair=logp_pair if self.paired_probes else None)
         self.inter[name] = float(new[0])
 
     def sweep(self):
@@ -392,6 +467,259 @@ class HDDM:
         for k, v in self.trace.items():
             out[k] = {"mean": float(np.mean(v)), "std": float(np.std(v)),
                       "2.5q": float(np.quantile(v, .025)), "97.5q": float(np.quantile(v, .975))}
+        return out
+
+
+class HDDMChains(HDDM):
+    """`chains` independent chains of HDDM(...) sampled in lockstep on one GPU.
+
+    HDDM's documented usage runs several chains (docs/source/howto.rst:267-291:
+    one model per chain, then kabuki's Gelman-Rubin R-hat) -- there, C
+    separate processes each making thousands of small likelihood calls. Here
+    the chains share the resident dataset and step together: every slice
+    evaluation of every chain is ONE wfpt_wiener_like_nodes_multi launch over
+    C parameter tables (2C for the paired stepping-out probes), so a launch
+    carries C x 100k trials of config 4 instead of 100k (one chain's call is
+    one wave round on the chip: DESIGN.md §10 "Launch-size floor").
+
+    The chains are independent Markov chains of the same model and step
+    methods as HDDM (each has its own coordinates and random numbers; a chain
+    whose slice is settled keeps evaluating its current point, whose value is
+    ignored). State arrays carry a leading chain axis: group[f] (C, levels),
+    std[f] (C,), subj[f] (C, units), inter[n] (C,); traces (kept, C).
+    """
+
+    def __init__(self, data, chains=4, **kw):
+        self.C = int(chains)
+        if self.C < 1:
+            raise ValueError("chains must be >= 1")
+        super().__init__(data, **kw)
+
+    def _init_values(self):
+        super()._init_values()  # HDDM's starting values (hddm_info.py:121-140), every chain
+        C = self.C
+        self.group = {k: np.tile(v, (C, 1)) for k, v in self.group.items()}
+        self.std = {k: np.full(C, float(v)) for k, v in self.std.items()}
+        self.subj = {k: np.tile(v, (C, 1)) for k, v in self.subj.items()}
+        self.inter = {k: np.full(C, float(v)) for k, v in self.inter.items()}
+
+    def node_tables(self, over=None):
+        """(C, n_nodes, 8) parameter tables of the chains at their current
+        values, the columns in `over` replaced ((C, units) per family, (C,)
+        for sv / sz / st)."""
+        key = tuple(self.subj[f].tobytes() for f in self.FAMILIES) + tuple(
+            self.inter[k].tobytes() for k in ("sv", "sz", "st"))
+        if getattr(self, "_tables_key", None) != key:
+            P = np.empty((self.C, self.n_nodes, 8))
+            P[:, :, 0] = self.subj["v"][:, self.node_unit["v"]]
+            P[:, :, 1] = self.inter["sv"][:, None]
+            P[:, :, 2] = self.subj["a"][:, self.node_unit["a"]]
+            P[:, :, 3] = 0.5
+            P[:, :, 4] = self.inter["sz"][:, None]
+            P[:, :, 5] = self.subj["t"][:, self.node_unit["t"]]
+            P[:, :, 6] = self.inter["st"][:, None]
+            P[:, :, 7] = self.p_outlier
+            self._tables, self._tables_key = P, key
+        if not over:
+            return self._tables
+        P = self._tables.copy()
+        for name, val in over.items():
+            col = self._COL[name]
+            val = np.asarray(val, dtype=np.float64)
+            P[:, :, col] = val[:, self.node_unit[name]] if name in self.FAMILIES else val[:, None]
+        return P
+
+    def node_logp_chains(self, overs):
+        """Per-node log-likelihoods of every chain for each override in
+        `overs`, one launch: (len(overs), C, n_nodes)."""
+        t0 = time.perf_counter()
+        tabs = np.concatenate([self.node_tables(o) for o in overs])
+        out = self.dataset.wiener_like_nodes_multi(tabs, **self.wp)
+        dt = time.perf_counter() - t0
+        self.likelihood_seconds += dt
+        self.likelihood_calls += 1
+        key = ",".join(sorted(overs[0])) + f" x{len(overs)}"
+        st = self.call_stats.setdefault(key, [0, 0.0])
+        st[0] += 1
+        st[1] += dt
+        return out.reshape(len(overs), self.C, self.n_nodes)
+
+    def node_logp(self, over=None):
+        return self.node_logp_chains([over or {}])[0]
+
+    def node_table(self, over=None):
+        raise NotImplementedError("HDDMChains: node_tables() holds one table per chain")
+
+    def _unit_group_c(self, fam):
+        """(C, units) group mean of each unit's level, per chain."""
+        nl = len(self.levels[fam])
+        return self.group[fam][:, np.arange(self.n_units[fam]) % nl]
+
+    def subj_prior_c(self, fam, x):
+        g = self._unit_group_c(fam)
+        sd = self.std[fam][:, None]
+        if fam == "v":
+            return normal_logpdf(x, g, sd)
+        return gamma_logpdf_mean_sd(x, g, sd)
+
+    def logp(self):
+        """Joint log density of the model at each chain's values: (C,)."""
+        lp = np.sum(self.node_logp(), axis=1)
+        for fam in self.FAMILIES:
+            lp = lp + np.sum(self.subj_prior_c(fam, self.subj[fam]), axis=1)
+        lp = lp + np.sum(self._group_prior("a", self.group["a"]), axis=1)
+        lp = lp + np.sum(self._group_prior("t", self.group["t"]), axis=1)
+        lp = lp + np.sum(normal_logpdf(self.group["v"], 2.0, 3.0), axis=1)
+        for f, s in (("a", 2.0), ("v", 2.0), ("t", 1.0)):
+            lp = lp + halfnormal_logpdf(self.std[f], s)
+        return lp
+
+    def _update_subject(self, fam):
+        C, nu = self.C, self.n_units[fam]
+        unit = self.node_unit[fam]
+        bins = (np.arange(C)[:, None] * nu + unit[None, :]).ravel()  # (chain, node) -> coordinate
+
+        def ll(rows):
+            return np.bincount(bins, weights=rows.ravel(), minlength=C * nu)
+
+        def prior(x):
+            return self.subj_prior_c(fam, x.reshape(C, nu)).ravel()
+
+        def logp(x):
+            r = self.node_logp_chains([{fam: x.reshape(C, nu)}])
+            return ll(r[0]) + prior(x)
+
+        def logp_pair(xl, xr):
+            r = self.node_logp_chains([{fam: xl.reshape(C, nu)}, {fam: xr.reshape(C, nu)}])
+            return ll(r[0]) + prior(xl), ll(r[1]) + prior(xr)
+
+        lower = 0.0 if fam in ("a", "t") else None
+        new, _ = slice_step(self.subj[fam].ravel(), logp, SLICE_WIDTHS[fam], self.rng,
+                            lower=lower, logp_pair=logp_pair if self.paired_probes else None)
+        self.subj[fam] = new.reshape(C, nu)
+
+    def _update_group(self, fam):
+        C, nl = self.C, len(self.levels[fam])
+        lv = np.arange(self.n_units[fam]) % nl
+        if fam == "v":  # kNormalNormal per chain and level (hddm_info.py:167-168)
+            tau0, mu0 = 3.0 ** -2, 2.0
+            tau = self.std["v"] ** -2
+            for k in range(nl):
+                xs = self.subj["v"][:, lv == k]
+                prec = tau0 + tau * xs.shape[1]
+                mean = (tau0 * mu0 + tau * xs.sum(axis=1)) / prec
+                self.group["v"][:, k] = self.rng.normal(mean, prec ** -0.5)
+        else:
+            def logp(g):
+                g = g.reshape(C, nl)
+                out = self._group_prior(fam, g)
+                for k in range(nl):
+                    xs = self.subj[fam][:, lv == k]
+                    out[:, k] = out[:, k] + np.sum(
+                        gamma_logpdf_mean_sd(xs, g[:, k:k + 1], self.std[fam][:, None]), axis=1)
+                return out.ravel()
+            new, _ = slice_step(self.group[fam].ravel(), logp, SLICE_WIDTHS[fam], self.rng,
+                                lower=0.0)
+            self.group[fam] = new.reshape(C, nl)
+        std_sd = {"a": 2.0, "v": 2.0, "t": 1.0}[fam]
+
+        def logp_std(s):
+            ok = s > 0
+            ss = np.where(ok, s, 1.0)[:, None]
+            g = self._unit_group_c(fam)
+            x = self.subj[fam]
+            ll = normal_logpdf(x, g, ss) if fam == "v" else gamma_logpdf_mean_sd(x, g, ss)
+            val = halfnormal_logpdf(np.where(ok, s, 1.0), std_sd) + np.sum(ll, axis=1)
+            return np.where(ok, val, -np.inf)
+
+        self.std[fam], _ = slice_step(self.std[fam].copy(), logp_std, SLICE_WIDTHS[fam + "_std"],
+                                      self.rng, lower=0.0)
+
+    def _update_inter(self, name):
+        prior = {"sv": lambda x: halfnormal_logpdf(x, 2.0), "sz": lambda x: beta_logpdf(x, 1, 3),
+                 "st": lambda x: halfnormal_logpdf(x, 0.3)}[name]
+        cur = self.inter[name]
+
+        def masked(x):
+            pr = prior(x)
+            ok = np.isfinite(pr)
+            # a probe outside the prior's support is not evaluated: the table
+            # keeps the chain's current value there and the result is -inf
+            return pr, ok, np.where(ok, x, cur)
+
+        def logp(x):
+            pr, ok, xv = masked(x)
+            r = self.node_logp_chains([{name: xv}])[0]
+            return np.where(ok, pr + np.sum(r, axis=1), -np.inf)
+
+        def logp_pair(xl, xr):
+            (pl, okl, vl), (pr_, okr, vr) = masked(xl), masked(xr)
+            r = self.node_logp_chains([{name: vl}, {name: vr}])
+            return (np.where(okl, pl + np.sum(r[0], axis=1), -np.inf),
+                    np.where(okr, pr_ + np.sum(r[1], axis=1), -np.inf))
+
+        self.inter[name], _ = slice_step(cur.copy(), logp, SLICE_WIDTHS[name], self.rng,
+                                         lower=0.0,
+                                         logp_pair=logp_pair if self.paired_probes else None)
+
+    def sample(self, iter, burn=0, thin=1, progress=None):
+        """Run `iter` lockstep sweeps of every chain; keep every `thin`-th
+        after `burn`. Returns traces (dict name -> (kept, C))."""
+        names = []
+        for fam in self.FAMILIES:
+            for k, lv in enumerate(self.levels[fam]):
+                names.append((f"{fam}" + (f"({','.join(map(str, lv))})" if lv else ""), fam, k))
+        trace = {nm: [] for nm, _, _ in names}
+        for fam in self.FAMILIES:
+            trace[f"{fam}_std"] = []
+        inter = [nm for nm in ("sv", "sz", "st") if nm in self.include]
+        for nm in inter:
+            trace[nm] = []
+        self.trace_subj = {f: [] for f in self.FAMILIES}
+        t0 = time.perf_counter()
+        for it in range(iter):
+            self.sweep()
+            if it >= burn and (it - burn) % thin == 0:
+                for nm, fam, k in names:
+                    trace[nm].append(self.group[fam][:, k].copy())
+                for fam in self.FAMILIES:
+                    trace[f"{fam}_std"].append(self.std[fam].copy())
+                    self.trace_subj[fam].append(self.subj[fam].copy())
+                for nm in inter:
+                    trace[nm].append(self.inter[nm].copy())
+            if progress and (it + 1) % progress == 0:
+                el = time.perf_counter() - t0
+                print(f"  [{it + 1}/{iter}] {el:.1f}s, {self.likelihood_calls} batched "
+                      f"likelihood calls ({self.C} chains)", flush=True)
+        self.trace = {k: np.asarray(v).reshape(-1, self.C) for k, v in trace.items()}
+        self.trace_subj = {k: np.asarray(v) for k, v in self.trace_subj.items()}
+        self.sample_seconds = time.perf_counter() - t0
+        return self.trace
+
+    def gen_stats(self):
+        """Posterior summaries pooled over the chains, with the Gelman-Rubin
+        R-hat of each node (kabuki.analyze.gelman_rubin's statistic)."""
+        out = {}
+        rh = self.gelman_rubin()
+        for k, v in self.trace.items():
+            flat = v.ravel()
+            out[k] = {"mean": float(np.mean(flat)), "std": float(np.std(flat)),
+                      "2.5q": float(np.quantile(flat, .025)),
+                      "97.5q": float(np.quantile(flat, .975)), "rhat": rh[k]}
+        return out
+
+    def gelman_rubin(self):
+        """R-hat per traced node: sqrt(((n - 1)/n W + B/n) / W) with W the mean
+        within-chain variance and B/n the variance of the chain means."""
+        out = {}
+        for k, v in self.trace.items():
+            n, C = v.shape
+            if C < 2 or n < 2:
+                out[k] = float("nan")
+                continue
+            W = float(np.mean(np.var(v, axis=0, ddof=1)))
+            Bn = float(np.var(np.mean(v, axis=0), ddof=1))
+            out[k] = float(np.sqrt(((n - 1) / n * W + Bn) / W)) if W > 0 else float("nan")
         return out
 
 

@@ -216,18 +216,21 @@ class Dataset:
         return kc[1]
 
     def _knobs_addr(self, err, n_st, n_sz, use_adaptive, simps_err, w_outlier):
-        """The cached knobs struct's address (it lives in self._kc)."""
+        """(knobs struct, its address). The caller keeps the struct in a local
+        until the raw call returns: another thread may replace self._kc (other
+        knobs) meanwhile, and the address must not outlive its struct."""
         self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
-        return self._kc[2]
+        kc = self._kc
+        return kc[1], kc[2]
 
     def wiener_like(self, v, sv, a, z, sz, t, st, err, n_st=10, n_sz=10, use_adaptive=1,
                     simps_err=1e-8, p_outlier=0, w_outlier=0.1):
         P = _lib.make_params(v, sv, a, z, sz, t, st, p_outlier)
-        kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        K, kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
         out = ctypes.c_double()
         c, h = self.ctx.handle, self.handle
         if not c or not h:  # closed: the C ABI's own argument error
-            _lib.check(_lib.wfpt_wiener_like(c, h, ctypes.byref(P), ctypes.byref(self._kc[1]),
+            _lib.check(_lib.wfpt_wiener_like(c, h, ctypes.byref(P), ctypes.byref(K),
                                              ctypes.byref(out)))
         rc = _lib.raw_wiener_like(c.value, h.value, ctypes.addressof(P), kaddr,
                                   ctypes.addressof(out))
@@ -322,14 +325,53 @@ class Dataset:
     def wiener_like_nodes_allreduce(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
                                     simps_err=1e-3, w_outlier=0.1):
         """Per-node sums over every rank's shard (hddm_amd.dist.init_comm):
-        one all-reduce of n_nodes + 1 doubles per call."""
-        table, keep = self._node_table(params)
+        one all-reduce of n_nodes + 1 doubles per call.
+
+        The exchange's count is the table's row count, which every rank
+        shares; whether this rank's dataset matches it (node ids present,
+        n_nodes rows) is checked by the library *inside* the collective, so a
+        rank with a bad dataset enters the all-reduce poisoned instead of
+        leaving its peers blocked in it."""
+        pm = np.ascontiguousarray(params, dtype=np.float64)
+        if pm.ndim != 2 or pm.shape[1] != 8:  # the table itself: the same on every rank
+            raise ValueError("params must have shape (n_nodes, 8)")
         K = self._knobs(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
-        out = np.empty(self.n_nodes, dtype=np.float64)
-        _lib.check(_lib.wfpt_wiener_like_nodes_allreduce(self.ctx.handle, self.handle, table,
-                                                         self.n_nodes, ctypes.byref(K),
-                                                         _lib.dptr(out)))
-        del keep
+        m = pm.shape[0]
+        out = np.empty(m, dtype=np.float64)
+        _lib.check(_lib.wfpt_wiener_like_nodes_allreduce(self.ctx.handle, self.handle,
+                                                         pm.ctypes.data_as(_lib._PP), m,
+                                                         ctypes.byref(K), _lib.dptr(out)))
+        return out
+
+    def wiener_like_nodes_multi(self, tables, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
+                                simps_err=1e-3, w_outlier=0.1, trials=False):
+        """T parameter tables in ONE launch: tables (T, n_nodes, 8) -> per-node
+        sums (T, n_nodes); row t equals wiener_like_nodes(tables[t]) bit for bit
+        (several MCMC chains in lockstep, or both stepping-out probes of a slice
+        step). trials=True: (sums, per-trial terms (T, n) in the caller's trial
+        order)."""
+        tb = np.ascontiguousarray(tables, dtype=np.float64)
+        if self.n_nodes == 0:
+            raise ValueError("dataset was created without node ids")
+        if tb.ndim != 3 or tb.shape[1:] != (self.n_nodes, 8) or tb.shape[0] < 1:
+            raise ValueError(f"tables must have shape (T, {self.n_nodes}, 8), T >= 1")
+        T = tb.shape[0]
+        K, kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+        out = np.empty((T, self.n_nodes), dtype=np.float64)
+        c, h = self.ctx.handle, self.handle
+        if trials:
+            terms = np.empty((T, self.n), dtype=np.float64)
+            _lib.check(_lib.wfpt_wiener_like_nodes_multi_ex(
+                c, h, tb.ctypes.data_as(_lib._PP), T, ctypes.byref(K), _lib.dptr(out),
+                _lib.dptr(terms)))
+            return out, terms
+        if not c or not h:  # closed: the C ABI's own argument error
+            _lib.check(_lib.wfpt_wiener_like_nodes_multi(c, h, tb.ctypes.data_as(_lib._PP), T,
+                                                         ctypes.byref(K), _lib.dptr(out)))
+        rc = _lib.raw_wiener_like_nodes_multi(c.value, h.value, tb.ctypes.data, T, kaddr,
+                                              out.ctypes.data)
+        if rc:
+            _lib.check(rc)
         return out
 
     def wiener_like_nodes(self, params, err=1e-4, n_st=2, n_sz=2, use_adaptive=1,
@@ -345,7 +387,7 @@ class Dataset:
                 raise ValueError("dataset was created without node ids")
             if pm.shape != (self.n_nodes, 8):
                 raise ValueError(f"params must have shape ({self.n_nodes}, 8)")
-            kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
+            K, kaddr = self._knobs_addr(err, n_st, n_sz, use_adaptive, simps_err, w_outlier)
             out = np.empty(self.n_nodes, dtype=np.float64)
             c, h = self.ctx.handle, self.handle
             if c and h:

@@ -14,6 +14,7 @@
  *   wfpt_pdf_array         <- wfpt.pdf_array           src/wfpt.pyx:32-48
  *   wfpt_full_pdf          <- wfpt.full_pdf (cpdef)    src/pdf.pxi:104-146
  *   wfpt_wiener_like_nodes <- one wfpt_like per PyMC node, batched
+ *   wfpt_wiener_like_nodes_multi <- the same for several parameter tables (chains)
  *                             hddm/likelihoods.py:52-73 via base.py:754-757
  *   wfpt_wiener_like_multi <- wfpt.wiener_like_multi   src/wfpt.pyx:244-274
  *   wfpt_dmat_cdf_array    <- cdfdif_wrapper.dmat_cdf_array
@@ -107,7 +108,10 @@ int wfpt_wiener_like_trials(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params 
                             const wfpt_knobs *k, double *out_logp, double *out_trial);
 /* perm[i] = the caller's index of the dataset's stored trial i (datasets are
  * stored grouped by node / boundary and ordered by |rt|; identity for
- * WFPT_DS_INPUT_ORDER). */
+ * WFPT_DS_INPUT_ORDER). An identity order is answered from the host, also after
+ * the dataset's context was closed; a stored permutation lives in device memory
+ * and needs the context (WFPT_ERR_ARG once it is closed). The copy is serialised
+ * with the context's calls. */
 int wfpt_dataset_order(const wfpt_ds *ds, int64_t *perm);
 /* Same on a host array (uploaded for this call). */
 int wfpt_wiener_like_host(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
@@ -123,6 +127,20 @@ int wfpt_wiener_like_nodes(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *
  * [0, 1] (wfpt.pyx:63-72 per node). */
 int wfpt_wiener_like_nodes_ex(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *per_node,
                               const wfpt_knobs *k, double *out_logp, double *out_trial);
+/* n_tables parameter tables over the same resident node dataset in ONE
+ * launch: tables[t * n_nodes + j] is node j's row in table t, out_logp[t *
+ * n_nodes + j] its sum. Replaces n_tables separate wfpt_like evaluations of
+ * every node (hddm/likelihoods.py:52-73, reached once per node per slice
+ * evaluation by the reference's samplers): several MCMC chains in lockstep
+ * (HDDM's multi-chain usage, docs/source/howto.rst:267-291) or both probes of
+ * a slice step's stepping-out. Table t's sums are bit for bit those of
+ * wfpt_wiener_like_nodes on table t alone. out_trial (nullable, n_tables x
+ * ds size): table t's per-trial terms at out_trial[t * n + i], caller order. */
+int wfpt_wiener_like_nodes_multi(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *tables,
+                                 int32_t n_tables, const wfpt_knobs *k, double *out_logp);
+int wfpt_wiener_like_nodes_multi_ex(wfpt_ctx *ctx, const wfpt_ds *ds, const wfpt_params *tables,
+                                    int32_t n_tables, const wfpt_knobs *k, double *out_logp,
+                                    double *out_trial);
 /* Per-trial mixture density, or its log if logp != 0 (wfpt.pyx:32-48). */
 int wfpt_pdf_array(wfpt_ctx *ctx, const double *x, int64_t n, const wfpt_params *p,
                    const wfpt_knobs *k, int logp, double *out);

@@ -220,6 +220,31 @@ def test_dataset_order_invariance_and_additivity(gpu, oracle_lib):
         assert_total(val, ref, "order/additivity")
 
 
+@pytest.mark.parametrize("n", [1000, 70_000, 300_000])
+def test_stored_order_is_the_stable_comparator_order(gpu, n):
+    """wfpt_dataset_create's stored order (radix sort above 64k trials, the
+    comparator sort below) is the stable sort by (boundary, |rt|, NaN last),
+    ties in input order; node datasets: by node, then |rt|. Inputs carry ties,
+    +-0, +-inf and NaNs (several payloads)."""
+    rng = np.random.default_rng(n)
+    x = np.round(rng.choice([-1.0, 1.0], n) * (0.3 + rng.gamma(2.0, 0.45, n)), 3)
+    k = max(n // 50, 4)
+    pos = rng.choice(n, 4 * k, replace=False)
+    x[pos[:k]] = np.nan
+    x[pos[k:k + 4]] = [0.0, -0.0, np.inf, -np.inf]
+    bits = x.view(np.uint64)
+    bits[pos[k + 4:2 * k]] |= 0x8000000000000000  # negative zero / sign flips
+    x[pos[2 * k:2 * k + 8]] = np.frombuffer(np.array(
+        [0x7ff8000000000001 + j for j in range(8)], dtype=np.uint64).tobytes(), dtype=np.float64)
+    nan = np.isnan(x)
+    ab = np.where(nan, 0.0, np.abs(x))
+    want = np.lexsort((np.arange(n), ab, nan, x > 0))
+    assert np.array_equal(gpu.Dataset(x).order(), want)
+    node = rng.integers(0, 97, n).astype(np.int32)
+    want_n = np.lexsort((np.arange(n), ab, nan, node))
+    assert np.array_equal(gpu.Dataset(x, node_id=node, n_nodes=97).order(), want_n)
+
+
 def test_nodes_match_per_node_wiener_like(gpu, oracle_lib):
     rng = np.random.default_rng(11)
     n_nodes = 37

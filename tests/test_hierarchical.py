@@ -143,6 +143,10 @@ class _OracleDataset:
                                         n_st, n_sz, use_adaptive, simps_err, po, w_outlier)
         return out
 
+    def wiener_like_nodes_multi(self, tables, **kw):
+        self.multi_calls = getattr(self, "multi_calls", 0) + 1
+        return np.stack([self.wiener_like_nodes(T, **kw) for T in tables])
+
 
 def test_model_bookkeeping_and_sweep_on_cpu(oracle_lib, monkeypatch):
     import pandas as pd
@@ -165,3 +169,99 @@ def test_model_bookkeeping_and_sweep_on_cpu(oracle_lib, monkeypatch):
     m.sample(6, burn=2)
     assert m.trace["v(hi)"].shape == (4,) and np.isfinite(m.logp())
     assert m.likelihood_calls > 6
+
+
+def _cpu_data(seed=2, n_subj=4, n=60):
+    import pandas as pd
+    rng = np.random.default_rng(seed)
+    rows = []
+    for s in range(n_subj):
+        for c, v in (("lo", 0.5), ("hi", 1.2)):
+            x = rng.choice([-1.0, 1.0], n, p=[0.3, 0.7]) * (0.3 + rng.gamma(2.0, 0.3, n))
+            rows.append(pd.DataFrame({"rt": x, "subj_idx": s, "cond": c}))
+    return pd.concat(rows, ignore_index=True)
+
+
+def test_slice_step_paired_probes_same_chain():
+    """slice_step with logp_pair (both stepping-out probes per call) gives
+    exactly the same draws as the one-side-at-a-time loop, with fewer calls."""
+    from hddm_amd.hierarchical import slice_step
+    n = 500
+    def lp(v):
+        lv = np.log(np.maximum(v, 1e-300))
+        return np.where(v > 0, -0.5 * (lv - 0.3) ** 2 / 0.04 - lv, -np.inf)
+    x_a = x_b = np.linspace(0.2, 3.0, n)
+    ra, rb = np.random.default_rng(7), np.random.default_rng(7)
+    ca = cb = 0
+    for _ in range(10):
+        x_a, k = slice_step(x_a, lp, 0.3, ra, lower=0.0)
+        ca += k
+        x_b, k = slice_step(x_b, lp, 0.3, rb, lower=0.0, logp_pair=lambda l, r: (lp(l), lp(r)))
+        cb += k
+        assert np.array_equal(x_a, x_b)
+    assert cb < ca
+
+
+@pytest.mark.parametrize("include", [(), ("sv", "sz", "st")])
+def test_paired_probes_keep_the_chain_on_cpu(oracle_lib, monkeypatch, include):
+    """HDDM's updates with the paired two-table probes (one
+    wiener_like_nodes_multi call for both stepping-out sides) sample the same
+    chain, bit for bit, as the one-table-per-probe updates."""
+    from hddm_amd import hierarchical as h
+    monkeypatch.setattr(h._wfpt, "Dataset", _OracleDataset)
+    data = _cpu_data()
+    traces = []
+    calls = []
+    for paired in (False, True):
+        m = h.HDDM(data, depends_on={"v": "cond"}, include=include, seed=0, paired_probes=paired)
+        m.sample(3)
+        traces.append(m.trace)
+        calls.append(m.likelihood_calls)
+    for k in traces[0]:
+        assert np.array_equal(traces[0][k], traces[1][k]), k
+    assert calls[1] < calls[0]
+
+
+def test_chains_bookkeeping_on_cpu(oracle_lib, monkeypatch):
+    """HDDMChains: C chains in lockstep, one multi-table call per slice
+    evaluation (2C tables for the paired probes), per-chain state and traces,
+    R-hat per node; a one-chain HDDMChains reproduces HDDM's chain."""
+    from hddm_amd import hierarchical as h
+    monkeypatch.setattr(h._wfpt, "Dataset", _OracleDataset)
+    data = _cpu_data(n=40)
+    m = h.HDDMChains(data, chains=3, depends_on={"v": "cond"}, include=("st",), seed=0)
+    T = m.node_tables()
+    assert T.shape == (3, 8, 8) and np.all(T[:, :, 7] == 0.05)
+    lp0 = m.logp()
+    assert lp0.shape == (3,) and np.all(np.isfinite(lp0)) and np.all(lp0 == lp0[0])
+    m.sample(4, burn=1)
+    assert m.trace["v(hi)"].shape == (3, 3) and m.trace["st"].shape == (3, 3)
+    assert m.trace_subj["a"].shape == (3, 3, 4)
+    assert m.dataset.multi_calls == m.likelihood_calls
+    assert np.all(np.isfinite(m.logp()))
+    st = m.gen_stats()
+    assert "rhat" in st["a"]
+    # chains differ (own random numbers), a one-chain HDDMChains is HDDM's chain
+    assert not np.array_equal(m.trace["a"][:, 0], m.trace["a"][:, 1])
+    one = h.HDDMChains(data, chains=1, depends_on={"v": "cond"}, include=("st",), seed=0)
+    one.sample(3)
+    ref = h.HDDM(data, depends_on={"v": "cond"}, include=("st",), seed=0)
+    ref.sample(3)
+    for k in ref.trace:
+        np.testing.assert_allclose(one.trace[k][:, 0], ref.trace[k], rtol=1e-12, atol=0, err_msg=k)
+
+
+@pytest.mark.gpu
+def test_chains_recover_parameters_small_model(gpu):
+    """4 lockstep chains on the GPU (multi-table node calls): the pooled
+    posterior recovers the group means and the chains agree (R-hat)."""
+    from hddm_amd.hierarchical import HDDMChains, gen_data
+    data, truth = gen_data(n_subj=12, n_trials=200, seed=9)
+    m = HDDMChains(data, chains=4, depends_on={"v": "cond"}, seed=1)
+    m.sample(150, burn=50)
+    st = m.gen_stats()
+    assert abs(st["a"]["mean"] - np.mean(truth["a"])) < 0.25
+    assert abs(st["t"]["mean"] - np.mean(truth["t"])) < 0.05
+    assert abs(st["v(c0)"]["mean"] - 0.5) < 0.35 and abs(st["v(c1)"]["mean"] - 1.0) < 0.35
+    for k in ("a", "t", "v(c0)", "v(c1)"):
+        assert st[k]["rhat"] < 1.2, (k, st[k]["rhat"])

@@ -494,30 +494,40 @@ def test_node_dataset_with_nan_rts(gpu, oracle_lib, family):
 @pytest.mark.parametrize("full", [False, True])
 def test_node_sums_never_stale(gpu, full):
     """The batched node call's per-node sums reach the mapped result slot
-    before its completion word. r05 first had every node's wave write its sum
-    straight to the slot; one full GPU-suite run then read a node sum of the
-    previous call. The publication now has a single writer and a system fence
-    before the word. This loop is the regression guard: alternating two
-    parameter tables, every call must return exactly the sums of its own
-    table (it did not reproduce the rare race on the old build in 550 calls:
-    a guard, not a proof)."""
-    from hddm_amd.hierarchical import HDDM, gen_data
-    inter = dict(sv=0.1, sz=0.1, st=0.1) if full else {}
-    data, truth = gen_data(n_subj=200, n_trials=500, **inter)
-    m = HDDM(data, depends_on={"v": "cond"}, include=tuple(inter), p_outlier=0.05)
-    A = m.node_table()
-    B = A.copy()
-    for j, (s, c) in enumerate(m.node_keys):
-        B[j, 0] = truth["v"][c][s]
-        B[j, 2] = truth["a"][s]
-        B[j, 5] = truth["t"][s]
-    ds = m.dataset
-    ra = ds.wiener_like_nodes(A, **m.wp).copy()
-    rb = ds.wiener_like_nodes(B, **m.wp).copy()
-    assert not np.array_equal(ra, rb)
-    reps = 150 if full else 400
-    for k in range(reps):
-        T, ref = (A, ra) if k % 2 == 0 else (B, rb)
-        r = ds.wiener_like_nodes(T, **m.wp)
-        bad = np.flatnonzero(r != ref)
-        assert bad.size == 0, (k, bad[:5], r[bad[:5]], ref[bad[:5]])
+    before its completion word (segment_publish_kernel: agent-scope sum
+    stores, an acq_rel ticket, a system-scope release of the word, the host's
+    acquire poll). Alternating two parameter tables over config 4's dataset,
+    every call must return exactly its own table's sums. That this loop can
+    see a late publication is shown by the next test, on a build whose sums
+    land after the word."""
+    import node_publication_check as npc
+    r = npc.run(full=full, reps=150 if full else 400)
+    assert r["tables_differ"] and r["sync_reads_agree"], r
+    assert r["stale_calls"] == 0, r
+
+
+@pytest.mark.gpu
+def test_stale_check_detects_late_publication(gpu):
+    """Sensitivity of test_node_sums_never_stale: the same loop in a child
+    process on the WFPT_PUB_DIAG build (built by __graft_entry__.build next to
+    the shipped library), whose non-last blocks store their nodes' sums ~70 us
+    after the completion word, must report stale calls -- the r05 failure
+    (a node sum of the previous call) made deterministic."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from hddm_amd import build as hb
+    lib = os.path.join(hb.LIBDIR, "libwfpt_amd_pubdiag.so")
+    assert os.path.exists(lib), "diagnostic build missing: run __graft_entry__.build()"
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, WFPT_AMD_LIB=lib)
+    p = subprocess.run([sys.executable, os.path.join(here, "node_publication_check.py"),
+                        "--full", "--reps", "20"], env=env, capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    print("diagnostic build:", r)
+    assert r["lib"] == "libwfpt_amd_pubdiag.so", r
+    assert r["tables_differ"] and r["sync_reads_agree"], r
+    assert r["stale_calls"] >= r["calls"] // 2, r

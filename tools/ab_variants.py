@@ -25,8 +25,7 @@ VARIANTS = {
     "stamps_noout": ["WFPT_NODE_DEBUG", "WFPT_NODE_DEBUG_NOOUT"],
     "recfence": ["WFPT_REC_FENCES=1"],
     "syncfence": ["WFPT_SYNC_FENCE=1"],
-    "pub_fence": ["WFPT_PUB_WT=0"],
-    "pub_direct": ["WFPT_PUB_DIRECT=1"],
+    "pub_diag": ["WFPT_PUB_DIAG=1"],
     "fastdbg": ["WFPT_NODE_DEBUG_FAST"],
     "ilp": ["-mllvm -amdgpu-sched-strategy=max-ilp"],
     "occbias": ["-mllvm -amdgpu-schedule-metric-bias=100"],
