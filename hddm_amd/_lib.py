@@ -139,7 +139,7 @@ wfpt_wiener_like_nodes_allreduce = _sig("wfpt_wiener_like_nodes_allreduce", _I,
 # WFPT_PATH_* (include/wfpt_amd.h): kernels the last likelihood call launched
 PATH_LEAN, PATH_ENGINE, PATH_SMALL, PATH_REDO = 1, 2, 4, 8
 PATH_FOLD, PATH_DIRECT, PATH_FIXED, PATH_SPLIT = 16, 32, 64, 128
-PATH_SMALL_SPLIT, PATH_NODE_SPLIT = 256, 512
+PATH_SMALL_SPLIT, PATH_NODE_SPLIT, PATH_NODE_RARE = 256, 512, 1024
 wfpt_decode_result = _sig("wfpt_decode_result", _I, [_PD, _PD])
 
 EXPORTED = [

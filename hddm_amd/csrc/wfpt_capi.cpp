@@ -146,6 +146,8 @@ struct wfpt_ctx {
   DevBuf<int> defer;         // dmat_cdf_array: deferred trial indices + count
   DevBuf<double> cdf_tab;    // dmat_cdf_array: the call's parameter-only tables
   DevBuf<int64_t> nd_idx;    // wiener_like_nodes: deferred trial indices
+  DevBuf<int64_t> rare_v;    // wiener_like_nodes: the rare trials (wfpt_kernels.hip: NodeRare)
+  DevBuf<int32_t> rare_j;
   DevBuf<wfpt::Params> nd_par;  // ... and their parameter rows
   DevBuf<int> nd_chunks;     // wiener_like_nodes: chunks the level-0 pass left to the chunk engine
   int* ncnt = nullptr;       // device [4]: the node path's listed chunks / records counters and
@@ -160,6 +162,8 @@ struct wfpt_ctx {
   double* mres_dev = nullptr;  // its device alias
   unsigned long long seq = 0;  // completion word finalize writes to mres[4]
   MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
+  DevBuf<wfpt::Params> dnodep;     // its device copy (node_table_dev: WFPT_NODE_TABLE_DEV=1)
+  bool node_table_dev = false;
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
   bool nodes_generic = false;  // WFPT_NODES=generic: per-trial generic node kernel only
@@ -696,6 +700,8 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* ns = std::getenv("WFPT_NODE_SPLIT")) c->node_split = std::strcmp(ns, "0") != 0;
   if (const char* nq = std::getenv("WFPT_NODE_SPEC")) c->node_spec = std::strcmp(nq, "0") != 0;
+  if (const char* nt = std::getenv("WFPT_NODE_TABLE_DEV"))
+    c->node_table_dev = std::strcmp(nt, "0") != 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
   if (const char* lm = std::getenv("WFPT_LEAN")) c->lean = std::strcmp(lm, "0") != 0;
   if (const char* sm = std::getenv("WFPT_SMALL")) c->small = std::strcmp(sm, "0") != 0;
@@ -763,6 +769,9 @@ void wfpt_close(wfpt_ctx* c) {
   c->defer.release();
   c->cdf_tab.release();
   c->nd_idx.release();
+  c->dnodep.release();
+  c->rare_v.release();
+  c->rare_j.release();
   c->nd_par.release();
   c->nd_chunks.release();
   if (c->n_defer) (void)hipFree(c->n_defer);
@@ -1081,7 +1090,7 @@ namespace {
 // selects, and the level-0 / chunk-engine / record kernels writing each
 // trial's term to c->lp.
 int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
-                 const wfpt::Knobs& K, int32_t n_tables = 1) {
+                 const wfpt::Knobs& K, wfpt::NodeSum* ns, int32_t n_tables = 1) {
   const int32_t m = d->n_nodes;
   const int64_t T = std::max<int32_t>(n_tables, 1);
   const int64_t rows = T * m;  // table t's node j at t m + j
@@ -1099,6 +1108,8 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
     HIP_TRY(c->nd_idx.reserve(std::max<int64_t>(T * d->n, 1)));
     HIP_TRY(c->nd_par.reserve(std::max<int64_t>(T * d->n, 1)));
     HIP_TRY(c->nd_chunks.reserve(std::max<int64_t>(T * ((d->n + 63) / 64), 1)));
+    HIP_TRY(c->rare_v.reserve(std::max<int64_t>(T * d->n, 1)));
+    HIP_TRY(c->rare_j.reserve(std::max<int64_t>(T * d->n, 1)));
   }
   // the split level 0 (adaptive t families, non-counting one-table calls):
   // the call's node rows + root z grids in device memory
@@ -1106,12 +1117,24 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
                      c->node_split && T == 1;
   wfpt::NodeTables nt{m, split, !c->count && c->node_spec};
   nt.n_tables = (int32_t)T;
+  nt.rare_v = c->rare_v.p;
+  nt.rare_j = c->rare_j.p;
+  *ns = wfpt::NodeSum{d->x, d->node, c->mnodep.d, &K, mode, c->rare_v.p, c->rare_j.p,
+                      c->count ? c->evals : nullptr, c->status};
   c->path = split ? WFPT_PATH_NODE_SPLIT : 0;
   HIP_TRY(c->mnode.reserve((size_t)rows + 2));
   HIP_TRY(c->lp.reserve(std::max<int64_t>(T * d->n, 1)));
   if (c->count) HIP_TRY(hipMemsetAsync(c->evals, 0, sizeof(unsigned long long), c->stream));
+  const wfpt::Params* table = c->mnodep.d;
+  if (c->node_table_dev && rows > 0) {  // one H2D copy instead of per-block mapped reads
+    HIP_TRY(c->dnodep.reserve(rows));
+    HIP_TRY(hipMemcpyAsync(c->dnodep.p, c->mnodep.h, rows * sizeof(wfpt::Params),
+                           hipMemcpyHostToDevice, c->stream));
+    table = c->dnodep.p;
+    ns->P = table;
+  }
   if (c->profile) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-  wfpt::launch_nodes(d->x, d->node, d->n, c->mnodep.d, K, mode, c->lp.p, c->nd_idx.p,
+  wfpt::launch_nodes(d->x, d->node, d->n, table, K, mode, c->lp.p, c->nd_idx.p,
                      c->nd_par.p, c->ncnt, c->nd_chunks.p, c->count ? c->evals : nullptr,
                      c->status, c->prof, c->stream, &nt);
   HIP_TRY(hipGetLastError());
@@ -1125,6 +1148,30 @@ int nodes_recover(wfpt_ctx* c, int rc) {
   (void)hipStreamSynchronize(c->stream);
   (void)hipMemset(c->ncnt, 0, 4 * sizeof(int));
   return rc;
+}
+
+// The per-node sums of the call's n_tables x n_nodes virtual nodes into the
+// mapped slot (segment_publish_kernel). A call whose kernels left rare trials
+// (the exact path, trees deeper than kTreeDepth: nearly never) is reported
+// pending by that launch; its rare trials are then settled (node_rare_kernel)
+// and the sums published again: one more host round trip, that call only.
+int nodes_publish(wfpt_ctx* c, const wfpt_ds* d, const wfpt::NodeSum& ns, int32_t n_tables) {
+  const int32_t m = d->n_nodes;
+  const int32_t rows = n_tables * m;
+  for (int pass = 0; pass < 2; ++pass) {
+    ++c->seq;
+    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->mnode.d, c->status, c->seq,
+                             c->stream, c->ncnt + 3, c->ncnt, n_tables, d->n, pass == 0);
+    if (hipGetLastError() != hipSuccess)
+      return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_publish_kernel launch failed"));
+    if (int rc = wait_word(c, c->mnode.h + rows + 1)) return nodes_recover(c, rc);
+    if (c->mnode.h[rows] != wfpt::kRarePendingHost) break;
+    c->path |= WFPT_PATH_NODE_RARE;
+    wfpt::launch_node_rare(c->lp.p, ns, c->ncnt, m, d->n, c->stream);
+    if (hipGetLastError() != hipSuccess)
+      return nodes_recover(c, fail(WFPT_ERR_HIP, "node_rare_kernel launch failed"));
+  }
+  return check_status_value(c->mnode.h[rows]);
 }
 
 int nodes_check(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node, const wfpt_knobs* k,
@@ -1146,17 +1193,12 @@ int wfpt_wiener_like_nodes_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* 
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
-  if (int rc = nodes_launch(c, d, per_node, K)) return nodes_recover(c, rc);
-  ++c->seq;
+  wfpt::NodeSum ns{};
+  if (int rc = nodes_launch(c, d, per_node, K, &ns)) return nodes_recover(c, rc);
   if (m > 0) {
     // per-node sums, status and the completion word land in mapped memory
     // (one launch; its last block resets the node counters)
-    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->mnode.d, c->status, c->seq,
-                             c->stream, c->ncnt + 3, c->ncnt);
-    if (hipGetLastError() != hipSuccess)
-      return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_publish_kernel launch failed"));
-    if (int rc = wait_word(c, c->mnode.h + m + 1)) return nodes_recover(c, rc);
-    if (int rc = check_status_value(c->mnode.h[m])) return rc;
+    if (int rc = nodes_publish(c, d, ns, 1)) return rc;
   } else {
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
@@ -1181,15 +1223,10 @@ int wfpt_wiener_like_nodes_multi_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_pa
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t rows = n_tables * m;
-  if (int rc = nodes_launch(c, d, tables, K, n_tables)) return nodes_recover(c, rc);
-  ++c->seq;
+  wfpt::NodeSum ns{};
+  if (int rc = nodes_launch(c, d, tables, K, &ns, n_tables)) return nodes_recover(c, rc);
   if (rows > 0) {
-    wfpt::launch_segment_sum(c->lp.p, d->off, m, c->res.p, c->mnode.d, c->status, c->seq,
-                             c->stream, c->ncnt + 3, c->ncnt, n_tables, d->n);
-    if (hipGetLastError() != hipSuccess)
-      return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_publish_kernel launch failed"));
-    if (int rc = wait_word(c, c->mnode.h + rows + 1)) return nodes_recover(c, rc);
-    if (int rc = check_status_value(c->mnode.h[rows])) return rc;
+    if (int rc = nodes_publish(c, d, ns, n_tables)) return rc;
   } else {
     if (hipStreamSynchronize(c->stream) != hipSuccess)
       return nodes_recover(c, fail(WFPT_ERR_HIP, "node pass failed on the device"));
@@ -1217,9 +1254,11 @@ int wfpt_wiener_like_nodes_local(wfpt_ctx* c, const wfpt_ds* d, const wfpt_param
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t m = d->n_nodes;
-  if (int rc = nodes_launch(c, d, per_node, K)) return nodes_recover(c, rc);
+  wfpt::NodeSum ns{};
+  if (int rc = nodes_launch(c, d, per_node, K, &ns)) return nodes_recover(c, rc);
   // every exit after nodes_launch restores the node counters (0 at rest)
-  wfpt::launch_segment_res(c->lp.p, d->off, m, c->res.p, c->status, false, c->stream, c->ncnt);
+  wfpt::launch_segment_res(c->lp.p, d->off, m, c->res.p, c->status, false, c->stream, c->ncnt,
+                           &ns);
   if (hipGetLastError() != hipSuccess)
     return nodes_recover(c, fail(WFPT_ERR_HIP, "segment_res launch failed"));
   if (hipMemcpyAsync(out, c->res.p, ((size_t)m + 1) * sizeof(double), hipMemcpyDeviceToHost,
@@ -1248,7 +1287,9 @@ int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_p
   if (lrc == WFPT_OK && d->n_nodes != n_nodes)
     lrc = fail(WFPT_ERR_ARG, "dataset has " + std::to_string(d->n_nodes) +
                                  " nodes, the call passes n_nodes = " + std::to_string(n_nodes));
-  if (lrc == WFPT_OK) lrc = nodes_launch(c, d, per_node, to_knobs(k));
+  const wfpt::Knobs K = k ? to_knobs(k) : wfpt::Knobs{};  // (null k: nodes_check failed)
+  wfpt::NodeSum ns{};
+  if (lrc == WFPT_OK) lrc = nodes_launch(c, d, per_node, K, &ns);
   // fault injection for the failure path's tests (WFPT_FAULT=nodes_allreduce_local:
   // this rank's per-node pass reports a failure after it was enqueued)
   if (lrc == WFPT_OK) {
@@ -1266,7 +1307,7 @@ int wfpt_wiener_like_nodes_allreduce(wfpt_ctx* c, const wfpt_ds* d, const wfpt_p
     }
   }
   wfpt::launch_segment_res(lrc == WFPT_OK ? c->lp.p : nullptr, lrc == WFPT_OK ? d->off : nullptr,
-                           m, c->res.p, c->status, lrc != WFPT_OK, c->stream, c->ncnt);
+                           m, c->res.p, c->status, lrc != WFPT_OK, c->stream, c->ncnt, &ns);
   if (hipGetLastError() != hipSuccess) {
     (void)ncclCommAbort(c->comm);
     c->comm = nullptr;

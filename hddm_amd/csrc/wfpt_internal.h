@@ -136,11 +136,35 @@ void launch_poison(double* res, hipStream_t s);
 // lp[t n, (t + 1) n), its deferred records carry virtual indices t n + i and
 // its listed chunks t ceil(n / 64) + c (d_idx / d_par up to T n records, clist
 // up to T ceil(n / 64) chunks).
+// rare_v / rare_j (T n entries each): the node path's rare trials (exact
+// path, trees deeper than kTreeDepth), counted in n_defer[1] and settled by
+// the summing kernel (launch_segment_sum / launch_segment_res, NodeSum).
 struct NodeTables {
   int32_t n_nodes;
   bool split, spec;
   int32_t n_tables = 1;
+  int64_t* rare_v = nullptr;
+  int32_t* rare_j = nullptr;
 };
+// What the summing kernels need to settle the rare trials before they sum:
+// the dataset, the call's (T x n_nodes) parameter table, the knobs and the
+// family (mode: the two-pass family; -1 / generic calls push none), evals
+// (nullable) for the exact path's evaluation counts.
+struct NodeSum {
+  const double* x;
+  const int32_t* node;
+  const Params* P;
+  const Knobs* K;
+  int mode;
+  int64_t* rare_v;
+  int32_t* rare_j;
+  unsigned long long* evals;
+  int* status;
+};
+// The rare trials of the call (counters[1] of them): each one's node term into
+// lp (exact path / per-lane walk). m: nodes per table, n: trials per table.
+void launch_node_rare(double* lp, const NodeSum& ns, int* counters, int32_t m, int64_t n,
+                      hipStream_t s);
 void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params* P,
                   const Knobs& K, int mode, double* lp, int64_t* d_idx, Params* d_par,
                   int* n_defer, int* clist, unsigned long long* evals, int* status, int* prof,
@@ -152,8 +176,9 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
 // status word is reset); then, after the exchange, res -> out[0, n_nodes] and
 // the completion word out[n_nodes + 1].
 // counters: the node path's n_defer words, reset to 0 (0 at rest)
-void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
-                        int* status, bool poison, hipStream_t s, int* counters);
+void launch_segment_res(double* lp, const int64_t* off, int32_t n_nodes, double* res,
+                        int* status, bool poison, hipStream_t s, int* counters,
+                        const NodeSum* ns);
 void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long long seq,
                         hipStream_t s);
 // One launch (segment_publish_kernel): the per-node sums into res, then the
@@ -161,9 +186,14 @@ void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long
 // and the completion word and resets counters[0..2] (0 at rest).
 // n_tables > 1: the T n_nodes sums of a multi-table call (table t's node j at
 // t n_nodes + j, its trials at t n + off[j] of lp; n = trials per table).
+// check_rare: a call with rare trials (counters[1] > 0) is not summed: out[T
+// n_nodes] = kRarePending (-1) and the completion word; the host then runs
+// launch_node_rare and this launch again with check_rare = 0.
+constexpr double kRarePendingHost = -1.0;
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s,
-                        int* ticket, int* counters, int32_t n_tables = 1, int64_t n = 0);
+                        int* ticket, int* counters, int32_t n_tables, int64_t n,
+                        int check_rare);
 // wiener_like_multi with a uniform adaptive / direct family (mode): level-0
 // pass + deferred trials (d_idx / d_par hold up to n records, *n_defer must
 // be 0 on the stream) into lp[n], then per-block sums into part / zeros

@@ -1023,12 +1023,29 @@ __device__ inline void eng_tables_wave(const Params& P, EngTables& T, int lane) 
 // A record's index is virtual (t n_tab + i: trial i of parameter table t, the
 // multi-table node call); its RT is x[i], its term lp[t n_tab + i].
 __device__ inline int64_t tab_trial(int64_t v, int64_t n_tab) { return v < n_tab ? v : v % n_tab; }
+// (the node path's rare list: see node_sum)
+constexpr int kRareShift = 56;
+constexpr int64_t kRareMask = (1LL << kRareShift) - 1;
+constexpr int kRareExact = 1, kRareWalk = 2;
+struct NodeRare {
+  int64_t* v;
+  int32_t* j;
+  int* n;
+};
+__device__ inline void rare_push(const NodeRare& R, int64_t v, int32_t vj, int kind, double* lp) {
+  const int k = atomicAdd(R.n, 1);
+  R.v[k] = v | ((int64_t)kind << kRareShift);
+  R.j[k] = vj;
+  lp[v] = 0.0;  // a neutral addend until the summing kernel settles the trial
+}
+
 template <int MODE, bool COUNT, bool MULTI>
 __device__ inline void node_records(ChunkLds<1>& cl, int lane, int w0, int nwaves,
                                     const double* x, const Knobs& K, double* lp,
                                     const int64_t* d_idx, const Params* d_par, int nd,
                                     unsigned long long* evals, int* status,
-                                    int64_t n_tab = INT64_MAX) {
+                                    int64_t n_tab = INT64_MAX, const NodeRare* R = nullptr,
+                                    const int32_t* node = nullptr, int32_t n_nodes = 0) {
   long long ne = 0;
   int errf = 0;
   for (int k = w0; k < nd; k += nwaves) {
@@ -1064,14 +1081,24 @@ __device__ inline void node_records(ChunkLds<1>& cl, int lane, int w0, int nwave
         tree_density<MODE, 1>(A, cl, 0, x0, p, defer, rf);
         if (COUNT) n1 = cl.cnt[0];
       }
-      if (defer) {
-        n1 = 0;
-        p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
-                              : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+      if constexpr (MULTI) {
+        if (defer) {
+          n1 = 0;
+          p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
+                                : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
+        }
+        ne += n1;
+        lp[i] = log_val(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier));
+      } else {
+        if (defer) {  // the node path's rare list (node_sum settles it)
+          const int64_t t = i / n_tab;
+          rare_push(*R, i, (int32_t)(t * n_nodes + node[i - t * n_tab]),
+                    (rf & kFlagExact) ? kRareExact : kRareWalk, lp);
+        } else {
+          ne += n1;
+          lp[i] = node_logp(p, Q, K);
+        }
       }
-      ne += n1;
-      lp[i] = MULTI ? log_val(p * (1 - Q.p_outlier) + (K.w_outlier * Q.p_outlier))
-                    : node_logp(p, Q, K);
     }
     wave_sync();  // the next record reuses this wave's LDS
   }
@@ -1614,38 +1641,86 @@ void launch_poison(double* res, hipStream_t s) {
   hipLaunchKernelGGL(poison_kernel, dim3(1), dim3(64), 0, s, res);
 }
 
-// One wave per node: sums per-trial log p of [off[j], off[j+1]) in fixed order.
-// res[j] = -inf if the node holds a zero-density trial (wfpt.pyx:71-72).
-__global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, const int64_t* off,
-                                                          int32_t n_nodes, double* res) {
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (j >= n_nodes) return;
-  const int64_t lo = off[j], hi = off[j + 1];
+// The node path's rare trials -- the exact path (near-ties, ambiguous series
+// decisions, densities below kExactBelow) and trees deeper than kTreeDepth --
+// are not settled by the level-0 / record / chunk kernels: they append the
+// trial to a list and leave lp[v] = +0.0, and the summing kernel settles each
+// node's rare trials (exact_pdf / fallback_pdf, one lane each) before it
+// publishes the node. Their code (wfpt_exact.hpp's double-double libm, the
+// per-lane walk's memory stack) is thus out of the hot kernels' registers and
+// scratch: node_fast_kernel<kDirect> 168 -> ~54 VGPRs (3 -> 8 waves/SIMD),
+// node_chunk_kernel without its 7.5 KB/lane of scratch.
+// Entry k: v[k] = virtual trial index (t n + i) | kind << kRareShift, j[k] =
+// its virtual node (t m + node[i]); *n the count (0 at rest: the summing
+// kernel's last block resets it).
+
+// Node vj's sum, one wave (vj = t m + jr: the trials [t n + off[jr],
+// t n + off[jr + 1]) of lp): each lane adds its strided terms in order, then
+// a wave_sum; -inf if any term is -inf (wfpt.pyx:71-72 per node). The rare
+// trials' terms are in lp by then (node_rare_kernel).
+__device__ inline double node_sum(const double* lp, const int64_t* off, int32_t vj, int32_t m,
+                                  int64_t n, int lane) {
+  const int tab = vj / m, jr = vj - tab * m;
+  const int64_t lo = tab * n + off[jr], hi = tab * n + off[jr + 1];
   double s = 0.0;
   int zero = 0;
-  for (int64_t i = lo + lane; i < hi; i += 64) {
-    const double v = lp[i];
-    if (v == -INFINITY) zero = 1;
-    else s += v;
+  // four strided terms per lane loaded together, then added in order (one
+  // memory latency per 256 trials instead of per 64)
+  for (int64_t i0 = lo + lane; i0 < hi; i0 += 256) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = i0 + 64 * u < hi ? lp[i0 + 64 * u] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (v[u] == -INFINITY) zero = 1;
+      else s += v[u];
+    }
   }
   s = wave_sum(s);
-  const bool anyz = __ballot(zero != 0) != 0ull;
-  if (lane == 0) res[j] = anyz ? -INFINITY : s;
+  return __ballot(zero != 0) != 0ull ? -INFINITY : s;
 }
 
-// One block: copies the per-node sums to the mapped host slot, then the
-// call's encoded error flags (out[n]) and, once all of it is visible, the
-// 64-bit completion word (out[n + 1]); resets the device status word.
-__global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, int32_t n,
-                                                            int* status, double* out,
-                                                            unsigned long long seq) {
-  for (int j = threadIdx.x; j < n; j += 256) out[j] = res[j];
-  __syncthreads();  // every thread's stores happen-before thread 0's release
-  if (threadIdx.x == 0) {
-    const int st = atomicExch(status, 0);
-    out[n] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
-    publish_word(reinterpret_cast<unsigned long long*>(out + n + 1), seq);
+// The rare trials of a node call (rare_push), one lane each: the exact path
+// or the per-lane walk of the trial's family, its node term into lp. Launched
+// only when the publication found the list non-empty (the host re-publishes;
+// a call with no rare trial -- nearly all of them -- never runs this code, and
+// its kernels carry neither its registers nor its scratch). n_tab: trials per
+// table, m: nodes per table (table t's node j at t m + j).
+__global__ __launch_bounds__(64, WFPT_SLOW_WAVES) void node_rare_kernel(NodeRare R, double* lp, const double* x,
+                                                          const Params* P, int32_t m,
+                                                          int64_t n_tab, Knobs K, int mode,
+                                                          int* status, unsigned long long* evals) {
+  const int nr = *R.n;
+  int errf = 0;
+  long long ne = 0;
+  for (int k = blockIdx.x * 64 + threadIdx.x; k < nr; k += gridDim.x * 64) {
+    const int64_t r = R.v[k];
+    const int64_t v = r & kRareMask;
+    const int kind = (int)(r >> kRareShift);
+    const int32_t vj = R.j[k];
+    const int64_t i = v - (int64_t)(vj / m) * n_tab;
+    const Params Q = P[vj];
+    long long n1 = 0;
+    double p;
+    if (kind == kRareExact) p = exact_pdf(x[i], Q, K, &n1, &errf);
+    else if (mode == kAdaptT) p = fallback_pdf<kAdaptT>(x[i], Q, K, &n1, &errf);
+    else if (mode == kAdaptZ) p = fallback_pdf<kAdaptZ>(x[i], Q, K, &n1, &errf);
+    else p = fallback_pdf<kAdaptTZ>(x[i], Q, K, &n1, &errf);
+    ne += n1;
+    lp[v] = node_logp(p, Q, K);
+  }
+  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
+  if (evals && ne) atomicAdd(evals, (unsigned long long)ne);
+}
+
+// One wave per node (grid-stride): the per-node sums into res (the node
+// all-reduce's vector and wfpt_wiener_like_nodes_local).
+__global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, const int64_t* off,
+                                                          int32_t n_nodes, double* res) {
+  const int lane = threadIdx.x & 63;
+  for (int j = blockIdx.x * 4 + (threadIdx.x >> 6); j < n_nodes; j += gridDim.x * 4) {
+    const double s = node_sum(lp, off, j, n_nodes, 0, lane);
+    if (lane == 0) res[j] = s;
   }
 }
 
@@ -1680,61 +1755,82 @@ __global__ __launch_bounds__(256) void publish_nodes_kernel(const double* res, i
 #ifndef WFPT_PUB_DIAG
 #define WFPT_PUB_DIAG 0
 #endif
+#ifndef WFPT_PUB_BLOCKS
+#define WFPT_PUB_BLOCKS 128
+#endif
+constexpr int32_t kPubBlocks = WFPT_PUB_BLOCKS;
 // Multi-table calls: n_nodes = T m virtual nodes, node j of table t at
 // t m + j, summing trials [t n + off[j], t n + off[j + 1]) of lp.
+// check_rare: a call whose level-0 / record / chunk kernels left rare trials
+// (*n_rare > 0) is not summed: the last block writes kRarePending in the
+// error slot and the completion word, the host runs node_rare_kernel and
+// launches this kernel again with check_rare = 0.
+constexpr double kRarePending = -1.0;  // (error counts are >= 0)
 __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, const int64_t* off,
                                                               int32_t n_nodes, int* status,
                                                               double* res, double* out,
                                                               unsigned long long seq, int* ticket,
                                                               int* counters, int32_t m_tab,
-                                                              int64_t n_tab) {
+                                                              int64_t n_tab, int check_rare) {
   __shared__ int last;
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  double sum = 0.0;
-  if (j < n_nodes) {
-    const int tab = j / m_tab, jr = j - tab * m_tab;
-    const int64_t lo = tab * n_tab + off[jr], hi = tab * n_tab + off[jr + 1];
-    double s = 0.0;
-    int zero = 0;
-    for (int64_t i = lo + lane; i < hi; i += 64) {
-      const double v = lp[i];
-      if (v == -INFINITY) zero = 1;
-      else s += v;
-    }
-    s = wave_sum(s);
-    const bool anyz = __ballot(zero != 0) != 0ull;
-    sum = anyz ? -INFINITY : s;
-    if (!WFPT_PUB_DIAG && lane == 0) {  // (1)
+  const int nwv = (int)gridDim.x * 4;  // waves; wave w sums nodes w, w + nwv, ...
+  const int j0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // (written by the call's earlier kernels: stream order)
+  const bool pending = check_rare && counters[1] > 0;
+  double sum = 0.0;  // (the diagnostic build's: one node per wave)
+  for (int j = pending ? n_nodes : j0; j < n_nodes; j += nwv) {
+    sum = node_sum(lp, off, j, m_tab, n_tab, lane);
+    if (!WFPT_PUB_DIAG && lane == 0)  // (1)
       __hip_atomic_store(&res[j], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // the storing wave waits for its agent-scope store to be performed:
-      // LLVM's workgroup barrier does not wait for other waves' vector
-      // stores (non-tgsplit gfx950 emits only lgkmcnt(0) before s_barrier),
-      // and thread 0's release below waits only for its own wave's
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
+  // the storing wave waits for its agent-scope stores (and status atomics) to
+  // be performed: LLVM's workgroup barrier does not wait for other waves'
+  // vector memory operations (non-tgsplit gfx950 emits only lgkmcnt(0) before
+  // s_barrier), and thread 0's release below waits only for its own wave's
+  if (!WFPT_PUB_DIAG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // (2)
   if (threadIdx.x == 0)  // (3)
     last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
            (int)gridDim.x - 1;
   __syncthreads();  // (4)
+  if (pending) {  // the host settles the rare trials and publishes again
+    if (!last) return;
+    if (threadIdx.x == 0) {
+      *ticket = 0;
+      out[n_nodes] = kRarePending;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+      publish_word(reinterpret_cast<unsigned long long*>(out + n_nodes + 1), seq);
+    return;
+  }
 #if WFPT_PUB_DIAG
   if (!last) {
     for (int r = 0; r < 20; ++r) __builtin_amdgcn_s_sleep(127);
-    if (j < n_nodes && lane == 0) out[j] = sum;  // after the word: stale reads follow
+    if (j0 < n_nodes && lane == 0) out[j0] = sum;  // after the word: stale reads follow
     return;
   }
-  if (j < n_nodes && lane == 0) out[j] = sum;
+  if (j0 < n_nodes && lane == 0) out[j0] = sum;
 #else
   if (!last) return;
-  for (int k = threadIdx.x; k < n_nodes; k += 256)
-    out[k] = __hip_atomic_load(&res[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // plain loads: every block's stores happen-before them (the acquire above
+  // invalidates this XCD's caches at agent scope); sixteen in flight per
+  // thread, then the stores (the compiler does not move a load of res above a
+  // store to out: they may alias)
+  for (int k0 = threadIdx.x; k0 < n_nodes; k0 += 16 * 256) {
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = k0 + 256 * u < n_nodes ? res[k0 + 256 * u] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      if (k0 + 256 * u < n_nodes) out[k0 + 256 * u] = v[u];
+  }
 #endif
   if (threadIdx.x == 0) {
     *ticket = 0;
     counters[0] = 0;
-    counters[1] = 0;
+    counters[1] = 0;  // the rare list's count
     counters[2] = 0;
     const int st = atomicExch(status, 0);
     out[n_nodes] = (double)(st & kFlagDepth) + ((st & kFlagBudget) ? kBudgetUnit : 0.0);
@@ -1843,7 +1939,7 @@ __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
                       double* lp, int64_t* d_idx, Params* d_par, int* n_defer, int* clist,
                       int* n_chunks, unsigned long long* evals, int* status, int* prof,
-                      int32_t n_nodes, int64_t nw_tab) {
+                      int32_t n_nodes, int64_t nw_tab, NodeRare R) {
 #ifdef WFPT_NODE_DEBUG_FAST
   const long long dbg_t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1852,6 +1948,7 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   // trials): its rows, its terms lp[t n + i], its records' virtual indices
   // t n + i and its chunks' ids t nw_tab + c
   const int64_t tab = blockIdx.y;
+  double* const lp0 = lp;
   P += tab * n_nodes;
   lp += tab * n;
   const int64_t vbase = tab * n, cbase = tab * nw_tab;
@@ -1882,8 +1979,9 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   long long ne = 0;
   bool defer = false;
   Params Q;
+  int nj = 0;
   if (i < n) {
-    const int nj = node[i];
+    nj = node[i];
     Q = staged ? rows[nj - first] : P[nj];
     double p, f[5];
     int flags = 0;
@@ -1904,19 +2002,12 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
   const unsigned long long b = __ballot(defer);
   if (b) {
     if (MODE == kDirect) {
-      // the rare exact-path trials settled on their own lane (node_slow_kernel's
-      // operations): no record, no second launch
+      // the rare exact-path trials (near-ties, densities below kExactBelow:
+      // fast_level0's kExact) go to the rare list; the summing kernel settles
+      // them with exact_pdf -- what full_pdf + settle gives such a trial
       if (defer) {
-        long long n1 = 0;
-        int f1 = 0;
-        const double xi = x[i];
-        double p = full_pdf<MODE, RegStack<2>>(xi, Q, K, n1, f1);
-        if (f1 & kFlagExact) p = __builtin_nan("");  // near-tie: settled exactly below
-        int fl = f1 & kFlagErrors;
-        p = settle(p, xi, Q, K, false, n1, fl);
-        if (fl & kFlagErrors) atomicOr(status, fl & kFlagErrors);
-        lp[i] = node_logp(p, Q, K);
-        if (COUNT) ne = n1;
+        rare_push(R, vbase + i, (int32_t)(tab * n_nodes + nj), kRareExact, lp0);
+        if (COUNT) ne = 0;  // (the summing kernel counts the exact path's evaluations)
       }
     } else {
       // the chunk for node_chunk_kernel and the trials as records for
@@ -2104,7 +2195,8 @@ __device__ inline void record_sync() {
 template <int MODE, int NW>
 __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTables& T, int wave,
                                         int lane, const double* x, const Knobs& K, double* lp,
-                                        int64_t i, const Params& Q, int& errf,
+                                        int64_t i, const Params& Q, const NodeRare& R,
+                                        double* lp_base, int64_t v, int32_t vj,
                                         long long dbg_entry = 0) {
   constexpr int NP = kTreePoints;
   constexpr int NG = MODE == kAdaptTZ ? 4 : 1;  // grids per t point
@@ -2243,12 +2335,12 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
       defer = false;
       p = 0.0;
     }
-    if (defer) {
-      long long n1 = 0;
-      p = (fl & kFlagExact) || fl == 0 ? exact_pdf(x0, Q, K, &n1, &errf)
-                                       : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
-    }
-    lp[i] = node_logp(p, Q, K);
+    // the rare list (node_sum settles it): the exact path, or the per-lane
+    // walk for a tree deeper than kTreeDepth
+    if (defer)
+      rare_push(R, v, vj, (fl & kFlagExact) || fl == 0 ? kRareExact : kRareWalk, lp_base);
+    else
+      lp[i] = node_logp(p, Q, K);
 #if defined(WFPT_NODE_DEBUG) && !defined(WFPT_NODE_DEBUG_NOOUT)
     // diagnostic builds: the record's phase times (100 MHz ticks: tables,
     // evaluations, z settlement, t tree + settlement) in place of its term
@@ -2286,12 +2378,19 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
 #ifndef WFPT_NODE_REC_TEAM
 #define WFPT_NODE_REC_TEAM 1
 #endif
+// Team records (one block each, ~12 us) while the call's records fit in one
+// round of resident blocks (2 per CU: the kernel's 68 KB of LDS); beyond, one
+// wave per record (~21 us, but 4x as many side by side): multi-table calls of
+// several chains defer thousands of trials
+#ifndef WFPT_REC_TEAM_MAX
+#define WFPT_REC_TEAM_MAX 512
+#endif
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
     unsigned long long* evals, int* status, int* prof, int spec, int32_t n_nodes,
-    int64_t nw_tab) {
+    int64_t nw_tab, NodeRare R) {
 #ifdef WFPT_NODE_DEBUG
   const long long dbg_entry = __builtin_amdgcn_s_memrealtime();
 #else
@@ -2308,35 +2407,35 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
   if (node_records_sparse(nrec, nc)) {  // a few deferred trials: one wave each
     if constexpr (!COUNT && (MODE == kAdaptT || MODE == kAdaptTZ)) {
       if (spec) {  // every tree point in two rounds (node_record_spec)
-        int errf = 0;
-        if (WFPT_NODE_REC_TEAM) {
+        if (WFPT_NODE_REC_TEAM && nrec <= WFPT_REC_TEAM_MAX) {
           // one block per record, its waves side by side (wave 0's LDS)
           ChunkLds<1>& c0 = lds[0];
           const int wv = threadIdx.x >> 6;
           for (int k = (int)blockIdx.x; k < nrec; k += (int)gridDim.x) {
             const int64_t v = r_idx[k];  // virtual: table t's trial i at t n + i
-            node_record_spec<MODE, kEngWaves>(c0.F, c0.X, c0.fl, c0.tab, wv, lane,
-                                              x + tab_trial(v, n), K, lp + v, 0, r_par[k], errf,
-                                              dbg_entry);
+            const int64_t t = v / n, ix = v - t * n;
+            node_record_spec<MODE, kEngWaves>(c0.F, c0.X, c0.fl, c0.tab, wv, lane, x + ix, K,
+                                              lp + v, 0, r_par[k], R, lp, v,
+                                              (int32_t)(t * n_nodes + node[ix]), dbg_entry);
           }
         } else {
           for (int k = w0; k < nrec; k += nwaves) {
             const int64_t v = r_idx[k];
-            node_record_spec<MODE, 1>(cl.F, cl.X, cl.fl, cl.tab, 0, lane, x + tab_trial(v, n), K,
-                                      lp + v, 0, r_par[k], errf,
+            const int64_t t = v / n, ix = v - t * n;
+            node_record_spec<MODE, 1>(cl.F, cl.X, cl.fl, cl.tab, 0, lane, x + ix, K, lp + v, 0,
+                                      r_par[k], R, lp, v, (int32_t)(t * n_nodes + node[ix]),
                                       dbg_entry);  // F: 1088 doubles, fl: 64 ints
           }
         }
-        if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
         return;
       }
     }
     node_records<MODE, COUNT, false>(cl, lane, w0, nwaves, x, K, lp, r_idx, r_par, nrec, evals,
-                                     status, n);
+                                     status, n, &R, node, n_nodes);
     return;
   }
   long long ne = 0;
-  int nseg = 0, nex = 0, nwk = 0, errf = 0;
+  int nseg = 0, nex = 0, nwk = 0;
   Tally ty;
   for (int k = w0; k < nc; k += nwaves) {
     const int64_t vc = clist[k];  // virtual: table t's chunk c at t nw_tab + c
@@ -2406,20 +2505,19 @@ __global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
         tree_density<MODE, 1>(A, cl, lane, x0, p, defer, rf);
         if (COUNT) n1 = cl.cnt[lane];
       }
-      if (defer) {  // rare: the exact path or the per-lane walk, on this lane
+      if (defer) {  // rare: the exact path or the per-lane walk, by node_sum
+        rare_push(R, tab * n + i, (int32_t)(tab * n_nodes + jn),
+                  (rf & kFlagExact) ? kRareExact : kRareWalk, lp);
         n1 = 0;
-        p = (rf & kFlagExact) ? exact_pdf(x0, Q, K, &n1, &errf)
-                              : fallback_pdf<MODE>(x0, Q, K, &n1, &errf);
         if (COUNT) ++((rf & kFlagExact) ? nex : nwk);
       }
-      if (mine) {
+      if (mine && !defer) {
         if (oc != kFinal) ne += n1;  // node_fast_kernel counted the trials it settled
         lpt[i] = node_logp(p, Q, K);
       }
       wave_sync();  // the next segment rebuilds this wave's LDS
     }
   }
-  if (errf & kFlagErrors) atomicOr(status, errf & kFlagErrors);
   if (COUNT) {
     ne = wave_sum_ll(ne);
     nex = (int)wave_sum_ll(nex);
@@ -2810,10 +2908,11 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
       split = true;
     }
   }
+  const NodeRare R{nt ? nt->rare_v : nullptr, nt ? nt->rare_j : nullptr, n_defer + 1};
   if (!split)
     hipLaunchKernelGGL((node_fast_kernel<MODE, COUNT>), dim3(blocks_for(n), T), dim3(kBlock), 0, s,
                        x, node, n, P, K, lp, d_idx, d_par, n_defer, clist, n_defer, evals, status,
-                       prof, m, nw);
+                       prof, m, nw, R);
   if constexpr (MODE != kDirect) {
     // adaptive families, one launch: the fast pass's records one wave each
     // when they are sparse in their chunks, else one wave per listed chunk
@@ -2821,7 +2920,7 @@ static void launch_nodes_two_pass(const double* x, const int32_t* node, int64_t 
     const int64_t nb = std::min<int64_t>((T * nw + kEngWaves - 1) / kEngWaves, 2048);
     hipLaunchKernelGGL((node_chunk_kernel<MODE, COUNT>), dim3(nb), dim3(kEngBlock), 0, s, x, node,
                        n, P, K, lp, clist, n_defer, d_idx, d_par, evals, status, prof,
-                       spec ? 1 : 0, m, nw);
+                       spec ? 1 : 0, m, nw, R);
   }
   // direct family: node_fast_kernel settles its exact-path trials itself
 }
@@ -2881,14 +2980,19 @@ void launch_nodes(const double* x, const int32_t* node, int64_t n, const Params*
   }
 }
 
-void launch_segment_res(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
-                        int* status, bool poison, hipStream_t s, int* counters) {
+void launch_segment_res(double* lp, const int64_t* off, int32_t n_nodes, double* res,
+                        int* status, bool poison, hipStream_t s, int* counters,
+                        const NodeSum* ns) {
   if (poison) {
     hipLaunchKernelGGL(node_poison_kernel, dim3(std::max<int32_t>((n_nodes + 255) / 256, 1)),
                        dim3(256), 0, s, res, n_nodes);
   } else if (n_nodes > 0) {
-    hipLaunchKernelGGL(segment_sum_kernel, dim3((n_nodes + 3) / 4), dim3(256), 0, s, lp, off,
-                       n_nodes, res);
+    // the all-reduce / local paths have no host round trip before their sums:
+    // the rare kernel always runs first (it exits at once on an empty list)
+    launch_node_rare(lp, *ns, counters, n_nodes, 0, s);
+    hipLaunchKernelGGL(segment_sum_kernel,
+                       dim3(std::min<int32_t>((n_nodes + 3) / 4, kPubBlocks)), dim3(256), 0, s,
+                       lp, off, n_nodes, res);
   }
   hipLaunchKernelGGL(node_status_kernel, dim3(1), dim3(64), 0, s, res, n_nodes, status,
                      poison ? 1 : 0, counters);
@@ -2899,13 +3003,25 @@ void launch_publish_vec(const double* res, int32_t n, double* out, unsigned long
   hipLaunchKernelGGL(publish_vec_kernel, dim3(1), dim3(256), 0, s, res, n, out, seq);
 }
 
+void launch_node_rare(double* lp, const NodeSum& ns, int* counters, int32_t m, int64_t n,
+                      hipStream_t s) {
+  const NodeRare R{ns.rare_v, ns.rare_j, counters + 1};
+  hipLaunchKernelGGL(node_rare_kernel, dim3(64), dim3(64), 0, s, R, lp, ns.x, ns.P, m, n, *ns.K,
+                     ns.mode, ns.status, ns.evals);
+}
+
 void launch_segment_sum(const double* lp, const int64_t* off, int32_t n_nodes, double* res,
                         double* out, int* status, unsigned long long seq, hipStream_t s,
-                        int* ticket, int* counters, int32_t n_tables, int64_t n) {
+                        int* ticket, int* counters, int32_t n_tables, int64_t n,
+                        int check_rare) {
   if (n_nodes <= 0) return;
   const int32_t nv = n_nodes * std::max(n_tables, 1);  // virtual nodes t m + j
-  hipLaunchKernelGGL(segment_publish_kernel, dim3((nv + 3) / 4), dim3(256), 0, s, lp, off, nv,
-                     status, res, out, seq, ticket, counters, n_nodes, n);
+  // one node per wave up to kPubBlocks blocks, then several per wave: the
+  // blocks' ticket releases serialise on one word (the diagnostic build keeps
+  // one node per wave)
+  const int32_t nb = WFPT_PUB_DIAG ? (nv + 3) / 4 : std::min<int32_t>((nv + 3) / 4, kPubBlocks);
+  hipLaunchKernelGGL(segment_publish_kernel, dim3(nb), dim3(256), 0, s, lp, off, nv, status, res,
+                     out, seq, ticket, counters, n_nodes, n, check_rare);
 }
 
 template <int MODE, bool COUNT>

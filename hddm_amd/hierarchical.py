@@ -82,7 +82,8 @@ def beta_logpdf(x, a, b):
 
 # ---------------------------------------------------------------- slice sampler
 
-def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_pair=None):
+def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_pair=None,
+               masked=False):
     """Vectorised univariate slice sampling (stepping out + shrinkage).
 
     x0: (n,) current values of n conditionally independent coordinates;
@@ -97,6 +98,11 @@ def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_
     random numbers the whole step -- are those of the side-by-side-free loop;
     only the number of calls drops (max of the two sides' steps instead of
     their sum).
+
+    masked=True: logp(x, active) and logp_pair(xl, xr, act_l, act_r) also get
+    the coordinates whose value the step will read; the others' results are
+    never used (a caller may skip evaluating them -- HDDMChains drops settled
+    chains' tables from the launch).
     """
     x0 = np.asarray(x0, dtype=np.float64)
     n = x0.size
@@ -122,6 +128,9 @@ def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_
         R = np.where(grow, R + w, R)
         return grow
 
+    def f1(x, act):
+        return logp(x, act) if masked else logp(x)
+
     if logp_pair is not None:
         act_l = np.ones(n, dtype=bool)
         act_r = np.ones(n, dtype=bool)
@@ -130,11 +139,12 @@ def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_
             do_l = steps_l < max_steps and act_l.any()
             do_r = steps_r < max_steps and act_r.any()
             if do_l and do_r:
-                fl, fr = logp_pair(np.where(act_l, L, x0), np.where(act_r, R, x0))
+                pl, pr = np.where(act_l, L, x0), np.where(act_r, R, x0)
+                fl, fr = logp_pair(pl, pr, act_l, act_r) if masked else logp_pair(pl, pr)
             elif do_l:
-                fl = logp(np.where(act_l, L, x0))
+                fl = f1(np.where(act_l, L, x0), act_l)
             elif do_r:
-                fr = logp(np.where(act_r, R, x0))
+                fr = f1(np.where(act_r, R, x0), act_r)
             else:
                 break
             calls += 1
@@ -149,7 +159,7 @@ def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_
             active = np.ones(n, dtype=bool)
             for _ in range(max_steps):
                 probe = np.where(active, L if side == 0 else R, x0)
-                f = logp(probe)
+                f = f1(probe, active)
                 calls += 1
                 grow = grow_left(active, f) if side == 0 else grow_right(active, f)
                 if not grow.any():
@@ -159,7 +169,7 @@ def slice_step(x0, logp, w, rng, lower=None, max_steps=50, max_shrink=200, logp_
     done = np.zeros(n, dtype=bool)
     for _ in range(max_shrink):
         cand = np.where(done, x1, L + rng.uniform(size=n) * (R - L))
-        f = logp(cand)
+        f = f1(cand, ~done)
         calls += 1
         acc = ~done & (f > y)
         x1 = np.where(acc, cand, x1)
@@ -503,10 +513,10 @@ class HDDMChains(HDDM):
         self.subj = {k: np.tile(v, (C, 1)) for k, v in self.subj.items()}
         self.inter = {k: np.full(C, float(v)) for k, v in self.inter.items()}
 
-    def node_tables(self, over=None):
+    def node_tables(self, over=None, idx=None):
         """(C, n_nodes, 8) parameter tables of the chains at their current
         values, the columns in `over` replaced ((C, units) per family, (C,)
-        for sv / sz / st)."""
+        for sv / sz / st); idx: only these chains' tables (len(idx), n_nodes, 8)."""
         key = tuple(self.subj[f].tobytes() for f in self.FAMILIES) + tuple(
             self.inter[k].tobytes() for k in ("sv", "sz", "st"))
         if getattr(self, "_tables_key", None) != key:
@@ -520,29 +530,57 @@ class HDDMChains(HDDM):
             P[:, :, 6] = self.inter["st"][:, None]
             P[:, :, 7] = self.p_outlier
             self._tables, self._tables_key = P, key
-        if not over:
+        if idx is None and not over:
             return self._tables
-        P = self._tables.copy()
-        for name, val in over.items():
+        P = self._tables.copy() if idx is None else self._tables[idx]
+        for name, val in (over or {}).items():
             col = self._COL[name]
             val = np.asarray(val, dtype=np.float64)
+            if idx is not None:
+                val = val[idx]
             P[:, :, col] = val[:, self.node_unit[name]] if name in self.FAMILIES else val[:, None]
         return P
 
-    def node_logp_chains(self, overs):
+    def node_logp_chains(self, overs, chains=None):
         """Per-node log-likelihoods of every chain for each override in
-        `overs`, one launch: (len(overs), C, n_nodes)."""
+        `overs`, one launch: (len(overs), C, n_nodes). chains (bool (C,),
+        optional): only these chains' tables go into the launch (a slice
+        step's settled chains are not evaluated; their rows are 0, unread)."""
         t0 = time.perf_counter()
-        tabs = np.concatenate([self.node_tables(o) for o in overs])
-        out = self.dataset.wiener_like_nodes_multi(tabs, **self.wp)
+        C, m = self.C, self.n_nodes
+        idx = None if chains is None or chains.all() else np.flatnonzero(chains)
+        out = np.zeros((len(overs), C, m))
+        if idx is not None and idx.size == 0:
+            return out
+        tabs = np.concatenate([self.node_tables(o, idx) for o in overs])
+        t1 = time.perf_counter()
+        # one launch per integration family: a table whose sz or st is 0 (a
+        # probe at the slice's lower bound) selects another family, and a
+        # launch over tables of several families takes the generic per-trial
+        # kernel (wfpt_capi.cpp: nodes_launch)
+        fam = (tabs[:, 0, 4] > 0).astype(np.int8) * 2 + (tabs[:, 0, 6] > 0)
+        if (fam == fam[0]).all():
+            r = self.dataset.wiener_like_nodes_multi(tabs, **self.wp)
+        else:
+            r = np.empty((tabs.shape[0], m))
+            for f in np.unique(fam):
+                sel = np.flatnonzero(fam == f)
+                r[sel] = self.dataset.wiener_like_nodes_multi(tabs[sel], **self.wp)
+        t2 = time.perf_counter()
+        if idx is None:
+            out = r.reshape(len(overs), C, m)
+        else:
+            out[:, idx] = r.reshape(len(overs), idx.size, m)
         dt = time.perf_counter() - t0
         self.likelihood_seconds += dt
+        self.device_call_seconds = getattr(self, "device_call_seconds", 0.0) + (t2 - t1)
         self.likelihood_calls += 1
+        self.tables_evaluated = getattr(self, "tables_evaluated", 0) + tabs.shape[0]
         key = ",".join(sorted(overs[0])) + f" x{len(overs)}"
         st = self.call_stats.setdefault(key, [0, 0.0])
         st[0] += 1
         st[1] += dt
-        return out.reshape(len(overs), self.C, self.n_nodes)
+        return out
 
     def node_logp(self, over=None):
         return self.node_logp_chains([over or {}])[0]
@@ -585,17 +623,23 @@ class HDDMChains(HDDM):
         def prior(x):
             return self.subj_prior_c(fam, x.reshape(C, nu)).ravel()
 
-        def logp(x):
-            r = self.node_logp_chains([{fam: x.reshape(C, nu)}])
+        def chains_of(act):
+            return act.reshape(C, nu).any(axis=1)
+
+        def logp(x, act=None):
+            r = self.node_logp_chains([{fam: x.reshape(C, nu)}],
+                                      None if act is None else chains_of(act))
             return ll(r[0]) + prior(x)
 
-        def logp_pair(xl, xr):
-            r = self.node_logp_chains([{fam: xl.reshape(C, nu)}, {fam: xr.reshape(C, nu)}])
+        def logp_pair(xl, xr, act_l=None, act_r=None):
+            ch = None if act_l is None else chains_of(act_l) | chains_of(act_r)
+            r = self.node_logp_chains([{fam: xl.reshape(C, nu)}, {fam: xr.reshape(C, nu)}], ch)
             return ll(r[0]) + prior(xl), ll(r[1]) + prior(xr)
 
         lower = 0.0 if fam in ("a", "t") else None
         new, _ = slice_step(self.subj[fam].ravel(), logp, SLICE_WIDTHS[fam], self.rng,
-                            lower=lower, logp_pair=logp_pair if self.paired_probes else None)
+                            lower=lower, logp_pair=logp_pair if self.paired_probes else None,
+                            masked=True)
         self.subj[fam] = new.reshape(C, nu)
 
     def _update_group(self, fam):
@@ -647,20 +691,23 @@ class HDDMChains(HDDM):
             # keeps the chain's current value there and the result is -inf
             return pr, ok, np.where(ok, x, cur)
 
-        def logp(x):
+        def logp(x, act=None):
             pr, ok, xv = masked(x)
-            r = self.node_logp_chains([{name: xv}])[0]
+            ch = ok if act is None else ok & act
+            r = self.node_logp_chains([{name: xv}], ch)[0]
             return np.where(ok, pr + np.sum(r, axis=1), -np.inf)
 
-        def logp_pair(xl, xr):
+        def logp_pair(xl, xr, act_l=None, act_r=None):
             (pl, okl, vl), (pr_, okr, vr) = masked(xl), masked(xr)
-            r = self.node_logp_chains([{name: vl}, {name: vr}])
+            ch = (okl | okr) if act_l is None else (okl & act_l) | (okr & act_r)
+            r = self.node_logp_chains([{name: vl}, {name: vr}], ch)
             return (np.where(okl, pl + np.sum(r[0], axis=1), -np.inf),
                     np.where(okr, pr_ + np.sum(r[1], axis=1), -np.inf))
 
         self.inter[name], _ = slice_step(cur.copy(), logp, SLICE_WIDTHS[name], self.rng,
                                          lower=0.0,
-                                         logp_pair=logp_pair if self.paired_probes else None)
+                                         logp_pair=logp_pair if self.paired_probes else None,
+                                         masked=True)
 
     def sample(self, iter, burn=0, thin=1, progress=None):
         """Run `iter` lockstep sweeps of every chain; keep every `thin`-th

@@ -307,6 +307,8 @@ int wfpt_debug_partials(wfpt_ctx *ctx, double *part, int32_t *zero, int64_t n);
                                      trial (small_split_kernel; with WFPT_PATH_SMALL) */
 #define WFPT_PATH_NODE_SPLIT 512  /* per-node call: t-node split level 0
                                      (node_grid_kernel + node_split_kernel) */
+#define WFPT_PATH_NODE_RARE 1024  /* per-node call: rare trials (exact path / deep trees)
+                                     settled by node_rare_kernel, sums published again */
 int wfpt_last_path(wfpt_ctx *ctx, int *path);
 int wfpt_synchronize(wfpt_ctx *ctx);
 

@@ -237,7 +237,8 @@ def test_chains_bookkeeping_on_cpu(oracle_lib, monkeypatch):
     m.sample(4, burn=1)
     assert m.trace["v(hi)"].shape == (3, 3) and m.trace["st"].shape == (3, 3)
     assert m.trace_subj["a"].shape == (3, 3, 4)
-    assert m.dataset.multi_calls == m.likelihood_calls
+    # one launch per slice evaluation (two when a probe at st = 0 splits the family)
+    assert m.likelihood_calls <= m.dataset.multi_calls < 1.1 * m.likelihood_calls
     assert np.all(np.isfinite(m.logp()))
     st = m.gen_stats()
     assert "rhat" in st["a"]

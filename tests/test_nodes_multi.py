@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from test_parity_summing import _seed3, assert_terms
-from test_parity_trials import node_terms_ref
+from test_parity_trials import KN, node_terms_ref
 
 pytestmark = pytest.mark.gpu
 
@@ -143,3 +143,54 @@ def test_multi_tables_mixed_families_and_errors(gpu):
         ds.wiener_like_nodes_multi(tabs[:, :-1])
     with pytest.raises(ValueError):
         gpu.Dataset(x).wiener_like_nodes_multi(tabs)
+
+
+@pytest.mark.parametrize("family", ["simple", "full", "st_only"])
+def test_rare_trials_settled_and_republished(gpu, oracle_lib, family):
+    """Trials the node kernels cannot settle -- densities below kExactBelow
+    without an outlier mixture to absorb them (RTs a hair above t, p_outlier
+    = 0), i.e. the exact path -- go to the rare list; the publication reports
+    the call pending, node_rare_kernel settles them and the sums are published
+    again (WFPT_PATH_NODE_RARE). Per trial against the reference, per node
+    against fsum, one- and multi-table calls bit-equal, and the next call
+    (no rare trial) is not pending."""
+    from hddm_amd import _lib
+    rng = np.random.default_rng({"simple": 21, "full": 22, "st_only": 23}[family])
+    n_nodes = 12
+    sizes = rng.integers(40, 120, n_nodes)
+    node = np.repeat(np.arange(n_nodes), sizes)
+    rng.shuffle(node)
+    t = 0.3
+    x = rng.choice([-1.0, 1.0], node.size) * (t + 0.4 + rng.gamma(2.0, 0.3, node.size))
+    close = rng.random(node.size) < 0.08  # a hair above t: tiny densities
+    x[close] = np.sign(x[close]) * (t + rng.uniform(2e-4, 2e-3, close.sum()))
+    P = np.zeros((n_nodes, 8))
+    P[:, 0] = rng.uniform(-1.5, 1.5, n_nodes)
+    P[:, 2] = rng.uniform(1.5, 2.5, n_nodes)
+    P[:, 3] = 0.5
+    P[:, 5] = t
+    if family == "full":
+        P[:, 1], P[:, 4], P[:, 6] = 0.3, 0.1, 1e-4
+    elif family == "st_only":
+        P[:, 6] = 1e-4
+    P[:, 7] = np.where(np.arange(n_nodes) % 2 == 0, 0.0, 0.05)  # no mixture on even nodes
+    ds = gpu.Dataset(x, node_id=node, n_nodes=n_nodes)
+    ctx = _lib.context()
+    sums, terms = ds.wiener_like_nodes(P, *KN, trials=True)
+    assert ctx.last_path() & _lib.PATH_NODE_RARE, "no rare trial reached the rare list"
+    ref = node_terms_ref(oracle_lib, x, node, P)
+    assert_terms(terms, ref, f"rare {family}")
+    for j in range(n_nodes):
+        rj = ref[node == j]
+        if np.isneginf(rj).any():
+            assert sums[j] == -np.inf
+        else:
+            assert abs(sums[j] - math.fsum(rj)) <= 1e-11 * math.fsum(np.abs(rj)) + 1e-12, j
+    assert np.array_equal(ds.wiener_like_nodes(P, *KN), sums)
+    multi = ds.wiener_like_nodes_multi(np.stack([P, P]), *KN)
+    assert np.array_equal(multi[0], sums) and np.array_equal(multi[1], sums)
+    P2 = P.copy()
+    P2[:, 7] = 0.05  # the mixture absorbs every tiny density: nothing rare
+    s2 = ds.wiener_like_nodes(P2, *KN)
+    assert not ctx.last_path() & _lib.PATH_NODE_RARE
+    assert np.all(np.isfinite(s2))

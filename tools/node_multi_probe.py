@@ -44,10 +44,19 @@ def main():
                 ds.wiener_like_nodes_multi(tabs, **m.wp)
             k_ms, nl, _ = ctx.profile_read(reset=True)
             ctx.profile(0)
+            ctx.profile(ctx.PROF_EVALS)
+            ctx.profile_lists(reset=True)
+            ds.wiener_like_nodes_multi(tabs, **m.wp)
+            _, _, ne = ctx.profile_read(reset=True)
+            lists = ctx.profile_lists(reset=True)
+            ctx.profile(0)
             med = float(np.median(ts)) * 1e6
             print(json.dumps({"full": full, "tables": T, "call_us_median": med,
                               "per_table_us": med / T, "node_kernels_us": k_ms / max(nl, 1) * 1e3,
-                              "trials_per_call": T * m.n_trials}), flush=True)
+                              "trials_per_call": T * m.n_trials,
+                              "evals_per_trial": ne / (T * m.n_trials),
+                              "records": lists.get("node_deferred"),
+                              "segments": lists.get("segments")}), flush=True)
         m.dataset.close()
 
 
