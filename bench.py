@@ -332,6 +332,30 @@ def c4_line(cpu_seconds=2.0):
             "cpu_port": {"kind": "port", "cores": 1, "per_node_call_s": per_node,
                          "sample": f"{reps} wiener_like calls on one 250-trial node"}}
         m.dataset.close()
+    # HDDM's multi-chain usage (docs/source/howto.rst:267-291): 8 chains of the
+    # full model in lockstep, every slice evaluation of every chain in one
+    # multi-table launch (hddm_amd.hierarchical.HDDMChains)
+    from hddm_amd.hierarchical import HDDMChains
+    data, _ = gen_data(n_subj=200, n_trials=500, dt=1e-4, sv=0.1, sz=0.1, st=0.1)
+    m = HDDMChains(data, chains=8, depends_on={"v": "cond"}, include=("sv", "sz", "st"),
+                   p_outlier=0.05, seed=1)
+    m.sample(20)
+    c0, s0 = m.likelihood_calls, m.likelihood_seconds
+    tb0 = m.tables_evaluated
+    t0 = time.perf_counter()
+    m.sample(2000)
+    el = time.perf_counter() - t0
+    calls = m.likelihood_calls - c0
+    rh = m.gelman_rubin()
+    out["full_8_chains"] = {
+        "sample_2000_s": el, "chain_sweeps_per_s": 8 * 2000 / el,
+        "batched_likelihood_calls_per_sweep": calls / 2000,
+        "tables_per_call": (m.tables_evaluated - tb0) / max(calls, 1),
+        "likelihood_us_per_call": (m.likelihood_seconds - s0) / max(calls, 1) * 1e6,
+        "likelihood_fraction_of_time": (m.likelihood_seconds - s0) / el,
+        "rhat_max_group_nodes": max(rh[k] for k in ("a", "t", "v(c0)", "v(c1)", "sv", "sz", "st")),
+        "vs_8_single_chain_runs": 8 * out["full"]["sample_2000_s"] / el}
+    m.dataset.close()
     return out
 
 

@@ -15,6 +15,7 @@
 #include <atomic>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -163,6 +164,12 @@ struct wfpt_ctx {
   unsigned long long seq = 0;  // completion word finalize writes to mres[4]
   MappedBuf<wfpt::Params> mnodep;  // per-node parameter table of wiener_like_nodes
   DevBuf<wfpt::Params> dnodep;     // its device copy (node_table_dev: WFPT_NODE_TABLE_DEV=1)
+  // WFPT_HOST_TIMING=1: host time of the multi-table node calls by phase
+  // (table rows, launches, wait, copy-out; ns summed), printed at wfpt_close
+  bool host_timing = false;
+  std::chrono::steady_clock::time_point ht_mark;
+  double ht[5] = {0, 0, 0, 0, 0};
+  int64_t ht_calls = 0;
   bool node_table_dev = false;
   MappedBuf<double> mnode;         // per-node sums + status + completion word
   bool spin = true;            // poll mres[3] instead of hipStreamSynchronize
@@ -700,6 +707,7 @@ int wfpt_open(int device, wfpt_ctx** out) {
   if (const char* nm = std::getenv("WFPT_NODES")) c->nodes_generic = std::strcmp(nm, "generic") == 0;
   if (const char* ns = std::getenv("WFPT_NODE_SPLIT")) c->node_split = std::strcmp(ns, "0") != 0;
   if (const char* nq = std::getenv("WFPT_NODE_SPEC")) c->node_spec = std::strcmp(nq, "0") != 0;
+  if (const char* ht = std::getenv("WFPT_HOST_TIMING")) c->host_timing = std::strcmp(ht, "0") != 0;
   if (const char* nt = std::getenv("WFPT_NODE_TABLE_DEV"))
     c->node_table_dev = std::strcmp(nt, "0") != 0;
   if (const char* fm = std::getenv("WFPT_FAST_ONLY")) c->fast_only = std::strcmp(fm, "0") != 0;
@@ -745,6 +753,13 @@ int wfpt_open(int device, wfpt_ctx** out) {
 
 void wfpt_close(wfpt_ctx* c) {
   if (!c) return;
+  if (c->host_timing && c->ht_calls > 0)
+    std::fprintf(stderr,
+                 "wfpt host timing over %lld multi-table node calls (us per call): rows %.1f, "
+                 "launches %.1f, wait %.1f, copy-out %.1f, total %.1f\n",
+                 (long long)c->ht_calls, c->ht[0] / c->ht_calls / 1e3, c->ht[1] / c->ht_calls / 1e3,
+                 c->ht[2] / c->ht_calls / 1e3, c->ht[3] / c->ht_calls / 1e3,
+                 c->ht[4] / c->ht_calls / 1e3);
   DeviceGuard g(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (wfpt_ds* d : c->dsets) {  // detached: destroying one later frees only its host part
@@ -1101,6 +1116,7 @@ int nodes_launch(wfpt_ctx* c, const wfpt_ds* d, const wfpt_params* per_node,
     const int mj = wfpt::select_mode(per_node[j].sz, per_node[j].st, K.use_adaptive);
     mode = (mode == -2 || mode == mj) ? mj : -1;
   }
+  if (c->host_timing) c->ht_mark = std::chrono::steady_clock::now();
   if (mode > wfpt::kAdaptTZ) mode = -1;  // fixed Simpson: generic kernel
   if (c->nodes_generic) mode = -1;
   HIP_TRY(c->res.reserve((size_t)rows + 1));
@@ -1223,8 +1239,11 @@ int wfpt_wiener_like_nodes_multi_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_pa
   std::lock_guard<std::mutex> lk(c->mu);
   DeviceGuard g(c->device);
   const int32_t rows = n_tables * m;
+  using clk = std::chrono::steady_clock;
+  const auto h0 = clk::now();
   wfpt::NodeSum ns{};
   if (int rc = nodes_launch(c, d, tables, K, &ns, n_tables)) return nodes_recover(c, rc);
+  const auto h1 = clk::now();
   if (rows > 0) {
     if (int rc = nodes_publish(c, d, ns, n_tables)) return rc;
   } else {
@@ -1233,7 +1252,20 @@ int wfpt_wiener_like_nodes_multi_ex(wfpt_ctx* c, const wfpt_ds* d, const wfpt_pa
     (void)hipMemset(c->ncnt, 0, 4 * sizeof(int));
   }
   if (int rc = finish_profile(c)) return rc;
+  const auto h2 = clk::now();
   std::memcpy(out, c->mnode.h, (size_t)rows * sizeof(double));
+  if (c->host_timing) {
+    const auto h3 = clk::now();
+    auto ns_ = [](clk::duration d_) {
+      return (double)std::chrono::duration_cast<std::chrono::nanoseconds>(d_).count();
+    };
+    c->ht[0] += ns_(c->ht_mark - h0);
+    c->ht[1] += ns_(h1 - c->ht_mark);
+    c->ht[2] += ns_(h2 - h1);
+    c->ht[3] += ns_(h3 - h2);
+    c->ht[4] += ns_(h3 - h0);
+    ++c->ht_calls;
+  }
   if (out_trial)
     for (int32_t t = 0; t < n_tables; ++t)
       if (int rc = trials_to_caller(d, c->lp.p + (int64_t)t * d->n, out_trial + (int64_t)t * d->n))

@@ -1632,11 +1632,15 @@ __device__ inline void tree_root(const Trial& tr, const Params& P, double& lb, d
 //           node's z integral needs refinement (bit k of `pend`: tree point
 //           k * kTreeW / 4); f[] = the root interval's values at lb, d, c, e, ub;
 //   kExact: the value hinges on last-bit rounding (recomputed exactly).
-template <int MODE, bool UNROLL = false>
+template <int MODE, bool UNROLL = false, bool KEEP_F = true>
 __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
                                  double& p, double (&f)[5], long long& ne, unsigned& pend);
 
-template <int MODE>
+// KEEP_F = false: f[] is not written (a caller that only needs p and the
+// outcome: the per-node level 0, whose deferred chunks redo their level 0);
+// the root Simpson sums are accumulated as the t nodes complete (the lean
+// pass's form: the same values, fewer live registers)
+template <int MODE, bool KEEP_F = true>
 __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, double& p,
                                   double (&f)[5], long long& ne, int& flags, unsigned& pend) {
   const Trial tr = trial_setup(x0, P);
@@ -1661,7 +1665,7 @@ __device__ inline int fast_level0(double x0, const Params& P, const Knobs& K, do
     G = zgrid_setup(z - tr.sz / 2., z + tr.sz / 2., v, sv, a);
   (void)t;
   (void)x;
-  return eng_level0<MODE, WFPT_FAST_L0_UNROLL != 0>(x0, P, K, G, p, f, ne, pend);
+  return eng_level0<MODE, WFPT_FAST_L0_UNROLL != 0, KEEP_F>(x0, P, K, G, p, f, ne, pend);
 }
 
 // The engine's level 0 (kAdaptT / kAdaptTZ): the same operations as
@@ -1853,10 +1857,10 @@ __device__ inline int eng_level0_t(const Trial& tr, const Params& P, const Knobs
   p = 0.0;
   return kFinal;
 }
-template <int MODE, bool UNROLL>
+template <int MODE, bool UNROLL, bool KEEP_F>
 __device__ inline int eng_level0(double x0, const Params& P, const Knobs& K, const ZGrid& G,
                                  double& p, double (&f)[5], long long& ne, unsigned& pend) {
-  return eng_level0_t<MODE, true, UNROLL>(trial_setup(x0, P), P, K, G, p, f, ne, pend);
+  return eng_level0_t<MODE, KEEP_F, UNROLL>(trial_setup(x0, P), P, K, G, p, f, ne, pend);
 }
 
 // z grids of the engine, relative to the dyadic points P of [lb_z, ub_z]:

@@ -1255,7 +1255,10 @@ __device__ inline void fin_write(double t, long long zz, int dd, int* status, do
 // order for a given (nb, G); G = 1 is the single-block order.
 constexpr int kFinLoads = 16;
 constexpr int kFinMaxBlocks = 64;
-constexpr int64_t kFinPerBlock = 8192;  // partials per block when split
+#ifndef WFPT_FIN_PER_BLOCK
+#define WFPT_FIN_PER_BLOCK 8192
+#endif
+constexpr int64_t kFinPerBlock = WFPT_FIN_PER_BLOCK;  // partials per block when split
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* part, const int* zeros,
                                                         int64_t nb, int defer_bits,
                                                         int* status, double* out,
@@ -1934,6 +1937,11 @@ __global__ __launch_bounds__(kBlock, WFPT_SLOW_WAVES) void node_kernel(
 // wave), which node_chunk_kernel completes 64 trials per wave. Direct family:
 // the rare exact-path trials are appended as (index, parameter row) records
 // for node_slow_kernel.
+// node_fast_kernel's level 0 without f[] (WFPT_NODE_KEEP_F=0; the deferred
+// chunks' level 0 is redone by node_chunk_kernel)
+#ifndef WFPT_NODE_KEEP_F
+#define WFPT_NODE_KEEP_F 1
+#endif
 template <int MODE, bool COUNT>
 __global__ __launch_bounds__(kBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K,
@@ -1994,7 +2002,7 @@ void node_fast_kernel(const double* x, const int32_t* node, int64_t n, const Par
       oc = eng_level0_t<MODE, false, true>(trial_setup_b(xi, Q, flip), Q, K, R.G[flip], p, f, ne,
                                            pend, WFPT_SIN_TABLE ? &R.S[flip][0][0] : nullptr);
     } else {
-      oc = fast_level0<MODE>(x[i], Q, K, p, f, ne, flags, pend);
+      oc = fast_level0<MODE, WFPT_NODE_KEEP_F != 0>(x[i], Q, K, p, f, ne, flags, pend);
     }
     if (oc == kFinal) lp[i] = node_logp(p, Q, K);
     else defer = true;
@@ -2385,8 +2393,12 @@ __device__ inline void node_record_spec(double* buf, double* tv, int* pf, EngTab
 #ifndef WFPT_REC_TEAM_MAX
 #define WFPT_REC_TEAM_MAX 512
 #endif
+// waves per SIMD the node chunk engine is compiled for (register budget)
+#ifndef WFPT_NODE_CHUNK_WAVES
+#define WFPT_NODE_CHUNK_WAVES 2
+#endif
 template <int MODE, bool COUNT>
-__global__ __launch_bounds__(kEngBlock, 2) void node_chunk_kernel(
+__global__ __launch_bounds__(kEngBlock, WFPT_NODE_CHUNK_WAVES) void node_chunk_kernel(
     const double* x, const int32_t* node, int64_t n, const Params* P, Knobs K, double* lp,
     const int* clist, const int* n_chunks, const int64_t* r_idx, const Params* r_par,
     unsigned long long* evals, int* status, int* prof, int spec, int32_t n_nodes,

@@ -527,6 +527,19 @@ def test_rccl_node_allreduce_failure_paths(gpu, monkeypatch):
                                                _lib.dptr(out))
     assert rc == 2
     assert np.array_equal(ds.wiener_like_nodes_allreduce(params), want)
+    # the same through the Python wrapper, which takes the count
+    # from the table (every rank's) and leaves the dataset checks to the
+    # library inside the collective: a mismatched table enters the exchange
+    # poisoned and fails after it (ValueError = WFPT_ERR_ARG), then the
+    # communicator works again
+    with pytest.raises(ValueError, match="nodes"):
+        ds.wiener_like_nodes_allreduce(big)
+    flat = gpu.Dataset(x)  # no node ids: also poisoned, inside the exchange
+    with pytest.raises(ValueError, match="node ids"):
+        flat.wiener_like_nodes_allreduce(params)
+    with pytest.raises(ValueError):  # not a table: refused before any collective
+        ds.wiener_like_nodes_allreduce(params[:, :7])
+    assert np.array_equal(ds.wiener_like_nodes_allreduce(params), want)
 
 
 def test_bench_launcher_does_not_touch_gpu():

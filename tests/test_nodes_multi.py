@@ -190,7 +190,7 @@ def test_rare_trials_settled_and_republished(gpu, oracle_lib, family):
     multi = ds.wiener_like_nodes_multi(np.stack([P, P]), *KN)
     assert np.array_equal(multi[0], sums) and np.array_equal(multi[1], sums)
     P2 = P.copy()
-    P2[:, 7] = 0.05  # the mixture absorbs every tiny density: nothing rare
+    P2[:, 5] = 0.1  # every RT well above t: no tiny density, nothing rare
     s2 = ds.wiener_like_nodes(P2, *KN)
     assert not ctx.last_path() & _lib.PATH_NODE_RARE
     assert np.all(np.isfinite(s2))

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--slow-dump", default=None,
                     help="save the data and the parameter table of the slowest batched "
                          "likelihood call (npz) here")
+    ap.add_argument("--no-pair", action="store_true",
+                    help="one table per stepping-out probe (no paired two-table calls)")
     ap.add_argument("--watchdog", type=float, default=0.0,
                     help="dump every thread's stack and exit after this many seconds")
     a = ap.parse_args()
@@ -60,7 +62,7 @@ def main():
     if a.progress:
         print(f"data: {len(data)} trials in {t_gen:.1f}s", flush=True)
     m = HDDM(data, depends_on={"v": "cond"}, include=("sv", "sz", "st") if a.full else (),
-             p_outlier=a.p_outlier, seed=1)
+             p_outlier=a.p_outlier, seed=1, paired_probes=not a.no_pair)
     if a.slow_dump:
         ds, inner, worst = m.dataset, m.dataset.wiener_like_nodes, [0.0]
 

@@ -22,11 +22,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--tables", default="1,2,4,8,16")
+    ap.add_argument("--full-only", action="store_true")
     a = ap.parse_args()
     from hddm_amd import _lib
     from test_nodes_multi import _c4, _chain_tables
     ctx = _lib.context(0)
-    for full in (True, False):
+    for full in ((True,) if a.full_only else (True, False)):
         m, _, start, P = _c4(full)
         ds = m.dataset
         for T in [int(v) for v in a.tables.split(",")]:

@@ -36,16 +36,27 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--engine-only", action="store_true",
+                    help="only the stress sets whose steady-state call runs engine_kernel, no C3 "
+                         "set (the PMC passes behind profiles/traffic_stress.json: every "
+                         "engine launch of the run is one of bench.py's engine sets)")
     a = ap.parse_args()
     from hddm_amd import _lib, wfpt
     ctx = _lib.context(0)
     rows = []
     sets = stress_sets(wfpt)
-    np.random.seed(20261015)
-    sets.append((wfpt.gen_rts_from_cdf(*FULL, samples=1_000_000, dt=1e-3), FULL))
+    if a.engine_only:
+        # bench.py's stress line: sets 0, 1, 3 take the engine, set 2 the lean
+        # pass (checked below: each kept set's calls run the engine)
+        sets = [sets[k] for k in (0, 1, 3)]
+    else:
+        np.random.seed(20261015)
+        sets.append((wfpt.gen_rts_from_cdf(*FULL, samples=1_000_000, dt=1e-3), FULL))
     for x, p in sets:
         ds = wfpt.Dataset(x)
         ds.wiener_like(*p, *KN)
+        if a.engine_only:
+            assert ctx.last_path() & _lib.PATH_ENGINE, "an --engine-only set took another path"
         ctx.profile(ctx.PROF_EVALS)
         ds.wiener_like(*p, *KN)
         _, _, ne = ctx.profile_read(reset=True)
