@@ -573,3 +573,26 @@ def test_bench_launcher_does_not_touch_gpu():
     assert "torch.distributed.run" in cmd and "--nproc-per-node=8" in cmd
     assert "--master-addr=127.0.0.1" in cmd
     assert loaded == "LOADED []", loaded
+
+
+def test_c5_shards_are_the_same_trials_at_every_world_size(monkeypatch):
+    """bench.py's C5 data: block b (C5_BLOCK trials) is sampled with seed
+    20261015 + b, and rank r of N takes its contiguous shard of the blocks'
+    concatenation, so every world size scores the same trials (value(N) /
+    c5_n1.value is a speed-up on one workload). Checked with small blocks and
+    a stand-in sampler (CPU)."""
+    import bench
+    from hddm_amd import dist as hdist
+
+    def fake_rts(n, seed):
+        return np.random.default_rng(seed).standard_normal(n)
+
+    monkeypatch.setattr(bench, "make_rts", fake_rts)
+    monkeypatch.setattr(bench, "C5_BLOCK", 1000)
+    total = 8 * 1000
+    whole = bench.c5_rts(0, total)
+    assert whole.size == total
+    assert np.array_equal(whole[3000:4000], fake_rts(1000, 20261015 + 3))
+    for world in (2, 3, 4, 8):
+        parts = [bench.c5_rts(*hdist.shard_range(total, world, r)) for r in range(world)]
+        assert np.array_equal(np.concatenate(parts), whole), world
