@@ -205,7 +205,11 @@ struct wfpt_ctx {
   std::vector<wfpt_ds*> dsets;
 };
 
-constexpr int64_t kSplitCap = 8192;  // heavy chunks a dataset records per call
+constexpr int64_t kSplitCap = 16384;  // heavy chunks a dataset records per call (both classes)
+// class-2 heavy chunks (Split::n2) are split while the dataset's heavy chunks
+// are at most 1 / kHeavyFewDiv of its chunks: then they are the launch's
+// tail; when many chunks are heavy, splitting them only adds waves
+constexpr int64_t kHeavyFewDiv = 16;
 
 struct wfpt_ds {
   wfpt_ctx* ctx = nullptr;
@@ -230,12 +234,13 @@ struct wfpt_ds {
   int split_cap = 0;
   unsigned char* hpred[2] = {nullptr, nullptr};
   int* hlist[2] = {nullptr, nullptr};
-  int* hcount = nullptr;  // [2]
+  int* hcount = nullptr;  // [4]: class 1 by parity, then class 2 by parity
   double* hlp = nullptr;
   int* hmeta = nullptr;
   int* hdone = nullptr;
   int* hzn = nullptr;
-  mutable int nsplit = 0;  // chunks the next call splits
+  mutable int nsplit = 0;  // class-1 chunks the next call splits
+  mutable int nsplit2 = 0; // class-2 chunks the next call splits
   mutable int parity = 0;
   // device: the caller's index of each stored trial (per-trial outputs of the
   // diagnostic calls are returned in the caller's order; kept in HBM, not in
@@ -364,6 +369,7 @@ wfpt::Split split_of(const wfpt_ds* d) {
   if (!d || !d->hcount) return S;
   const int cur = d->parity, nx = 1 - cur;
   S.n = d->nsplit;
+  S.n2 = d->nsplit2;
   S.cap = d->split_cap;
   S.list = d->hlist[cur];
   S.pred = d->hpred[cur];
@@ -383,9 +389,13 @@ void split_advance(const wfpt_ds* d, bool engine, const double* r) {
   if (!d) return;
   if (!engine || !d->hcount) {
     d->nsplit = 0;
+    d->nsplit2 = 0;
     return;
   }
-  d->nsplit = (int)std::min<double>(r[5], (double)d->split_cap);
+  const int half = d->split_cap / 2;
+  d->nsplit = (int)std::min<double>(r[5], (double)half);
+  const int n2 = (int)std::min<double>(r[7], (double)half);
+  d->nsplit2 = (int64_t)(d->nsplit + n2) * kHeavyFewDiv <= d->nw ? n2 : 0;
   d->parity = 1 - d->parity;
 }
 
@@ -446,7 +456,7 @@ int run_sum(wfpt_ctx* c, const double* dx, int64_t n, const wfpt::Params& P,
       c->path |= direct ? WFPT_PATH_DIRECT
                         : (part & wfpt::kPassLean)
                               ? WFPT_PATH_LEAN
-                              : (WFPT_PATH_ENGINE | (S.n > 0 ? WFPT_PATH_SPLIT : 0));
+                              : (WFPT_PATH_ENGINE | (S.n + S.n2 > 0 ? WFPT_PATH_SPLIT : 0));
     if (!direct && (part & wfpt::kPassRedo)) c->path |= WFPT_PATH_REDO;
     if (part & wfpt::kPassDeferred) c->path |= WFPT_PATH_FOLD;
   }
@@ -897,8 +907,8 @@ int wfpt_dataset_create_ex(wfpt_ctx* c, const double* rt, int64_t n, const int32
     if (e == hipSuccess) e = hipMemset(d->hpred[k], 0, nwb);
     if (e == hipSuccess) e = hipMalloc((void**)&d->hlist[k], d->split_cap * sizeof(int));
   }
-  if (e == hipSuccess) e = hipMalloc((void**)&d->hcount, 2 * sizeof(int));
-  if (e == hipSuccess) e = hipMemset(d->hcount, 0, 2 * sizeof(int));
+  if (e == hipSuccess) e = hipMalloc((void**)&d->hcount, 4 * sizeof(int));
+  if (e == hipSuccess) e = hipMemset(d->hcount, 0, 4 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&d->hlp, (size_t)d->split_cap * 64 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&d->hmeta, (size_t)d->split_cap * 64 * sizeof(int));
   if (e == hipSuccess) e = hipMalloc((void**)&d->hdone, d->split_cap * sizeof(int));
@@ -1639,10 +1649,11 @@ void ar_reset(wfpt_ctx* c, const wfpt_ds* d) {
   if (!d) return;
   (void)hipStreamSynchronize(c->stream);
   d->nsplit = 0;
+  d->nsplit2 = 0;
   d->no_defer = false;
   d->no_tree = false;
   d->tree_frac = 1.0;
-  if (d->hcount) (void)hipMemset(d->hcount, 0, 2 * sizeof(int));
+  if (d->hcount) (void)hipMemset(d->hcount, 0, 4 * sizeof(int));
 }
 }  // namespace
 

@@ -40,19 +40,27 @@ constexpr int kPhaseWaves = 16384;
 // (next_*); the following call splits those chunks into kSplit units of
 // kSplitTrials trials, one wave each. All pointers null / n = 0: no split, no
 // record (host arrays, non-engine families).
-constexpr int kSplit = 8, kSplitTrials = 64 / kSplit;
+#ifndef WFPT_SPLIT
+#define WFPT_SPLIT 8  // units per heavy chunk (kSplitTrials trials each)
+#endif
+constexpr int kSplit = WFPT_SPLIT, kSplitTrials = 64 / kSplit;
+// Two classes (WFPT_HEAVY_TOTAL): 1 = more than kHeavyZ z walks after level
+// 0 (always split), 2 = more than kHeavyZ over all levels only (split while
+// the dataset has few heavy chunks: the host sets n2 = 0 otherwise). The
+// lists hold class 1 in [0, cap / 2) and class 2 in [cap / 2, cap).
 struct Split {
-  int n;                       // chunks split in this call (their units come first)
+  int n;                       // class-1 chunks split in this call (their units come first)
+  int n2;                      // class-2 chunks split in this call (units after class 1's)
   int cap;                     // capacity of the chunk lists and per-chunk state
-  const int* list;             // [n] their chunk ids
-  const unsigned char* pred;   // [chunks] 1 = split in this call
+  const int* list;             // [cap] their chunk ids (class 1 from 0, class 2 from cap / 2)
+  const unsigned char* pred;   // [chunks] 1 / 2 = recorded heavy of that class last call
   unsigned char* next_pred;    // [chunks] this call's record for the next call
   int* next_list;              // [cap]
-  int* next_n;                 // device counter (0 at the call's start)
+  int* next_n;                 // device counters [0] class 1, [2] class 2 (0 at the call's start)
   double* lp;                  // [cap * 64] per-trial log terms of split chunks
   int* meta;                   // [cap * 64] zero | defer << 1 | rflag << 2
   int* done;                   // [cap] units finished (0 at rest)
-  int* zn;                     // [cap] level-0 z walks summed over units (0 at rest)
+  int* zn;                     // [cap] z walks summed over units: level 0 | all levels << 16
 };
 
 // Error flags encoded as counts in one double that survives an RCCL sum:

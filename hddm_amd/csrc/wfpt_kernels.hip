@@ -282,6 +282,12 @@ void direct_kernel(TrialArgs A, Work W, DirectArgs D) {
 #ifndef WFPT_HEAVY_Z
 #define WFPT_HEAVY_Z 96
 #endif
+// WFPT_HEAVY_TOTAL=1: a chunk with more than kHeavyZ z walks over all its
+// levels (not after level 0 alone) is heavy too: class 2, split while the
+// dataset has few heavy chunks (Split::n2)
+#ifndef WFPT_HEAVY_TOTAL
+#define WFPT_HEAVY_TOTAL 1
+#endif
 constexpr int kEngBlock = WFPT_ENG_BLOCK;
 constexpr int kEngWaves = kEngBlock / 64;
 constexpr int kHeavyZ = WFPT_HEAVY_Z;
@@ -688,17 +694,23 @@ __device__ inline void tally_out(const Work& W, const Tally& ty) {
 }
 
 // Records chunk c for the next call's split (lane 0 of its last wave).
-__device__ inline void record_heavy(const Split& S, int64_t c, bool heavy) {
+__device__ inline void record_heavy(const Split& S, int64_t c, int cls) {
   if (!S.next_pred) return;
   unsigned char flag = 0;
-  if (heavy) {
-    const int slot = atomicAdd(S.next_n, 1);
-    if (slot < S.cap) {
-      S.next_list[slot] = (int)c;
-      flag = 1;
+  if (cls) {
+    const int half = S.cap / 2;
+    const int slot = atomicAdd(S.next_n + (cls == 2 ? 2 : 0), 1);
+    if (slot < half) {
+      S.next_list[(cls == 2 ? half : 0) + slot] = (int)c;
+      flag = (unsigned char)cls;
     }
   }
   S.next_pred[c] = flag;
+}
+// Heavy class of a chunk from its z walks after level 0 (z0) and over all
+// levels (zt): 1, 2 (WFPT_HEAVY_TOTAL) or 0.
+__device__ inline int heavy_class(int z0, int zt) {
+  return z0 > kHeavyZ ? 1 : ((WFPT_HEAVY_TOTAL && zt > kHeavyZ) ? 2 : 0);
 }
 
 // Chunk outputs of a split unit's trials: per-trial outputs now, the chunk
@@ -708,8 +720,8 @@ __device__ inline void record_heavy(const Split& S, int64_t c, bool heavy) {
 template <int MODE, bool COUNT, int OUT>
 __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split& S,
                                  const ChunkLds<1>& cl, int slot, int sub, int lane, double x0,
-                                 int nz0) {
-  const int64_t c = S.list[slot];
+                                 int nz0, int nzt) {
+  const int64_t c = S.list[slot < S.n ? slot : S.cap / 2 + (slot - S.n)];
   const int64_t i = c * 64 + sub * kSplitTrials + lane;
   const bool own = lane < kSplitTrials && i < A.n;
   double p = 0.0, lp = 0.0;
@@ -730,7 +742,7 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   int prev = 0;
   if (lane == 0) {
-    atomicAdd(&S.zn[slot], nz0);
+    atomicAdd(&S.zn[slot], nz0 + (nzt << 16));
     prev = __hip_atomic_fetch_add(&S.done[slot], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   prev = __shfl(prev, 0, 64);
@@ -750,7 +762,7 @@ __device__ inline void split_out(const TrialArgs& A, const Work& W, const Split&
   }
   if (lane == 0) {
     const int znc = __hip_atomic_load(&S.zn[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    record_heavy(S, c, znc > kHeavyZ);
+    record_heavy(S, c, heavy_class(znc & 0xffff, znc >> 16));
     S.done[slot] = 0;
     S.zn[slot] = 0;
   }
@@ -771,10 +783,15 @@ __global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(Trial
   // work units: the split chunks' units first (dispatched first), then one
   // wave per chunk
   const int64_t u = (int64_t)blockIdx.x * kEngWaves + (threadIdx.x >> 6);
-  const bool split = u < (int64_t)S.n * kSplit;
+  const int ns = S.n + S.n2;  // split chunks: class 1's units, then class 2's
+  const bool split = u < (int64_t)ns * kSplit;
   const int slot = split ? (int)(u / kSplit) : 0, sub = split ? (int)(u % kSplit) : 0;
-  const int64_t c = split ? (int64_t)S.list[slot] : u - (int64_t)S.n * kSplit;
-  if (!split && (c * 64 >= A.n || (S.n > 0 && S.pred[c]))) return;  // past the end / split
+  const int64_t c = split ? (int64_t)S.list[slot < S.n ? slot : S.cap / 2 + (slot - S.n)]
+                          : u - (int64_t)ns * kSplit;
+  // past the end / split in this call (class 2 only while n2 > 0)
+  if (!split && (c * 64 >= A.n ||
+                 (ns > 0 && (S.pred[c] == 1 || (S.pred[c] == 2 && S.n2 > 0)))))
+    return;
   if (W.redo && !W.redo[c]) return;  // redo pass: only the chunks the lean pass flagged
   load_tables(cl, tab, lane);
   const int64_t i = split ? c * 64 + sub * kSplitTrials + lane : c * 64 + lane;
@@ -834,7 +851,7 @@ __global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(Trial
     rounds = true;
   }
   Tally ty;
-  int nz0 = 0;
+  int nz0 = 0, nzt = 0;
   if (rounds) {
     // chunks that refined in-wave (a split chunk once: its unit 0); finalize
     // reports the count, which picks the next call's level-0 pass
@@ -844,14 +861,25 @@ __global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(Trial
     pc.mark(1);
     refine_rounds<MODE, COUNT, 1>(A, cl, lane, stage, ty, pc);
     if (split) nz0 = ty.z[0];
+    nzt = ty.z[0] + ty.z[1] + ty.z[2];  // the z walks of every level
   }
   if (split) {
-    split_out<MODE, COUNT, OUT>(A, W, S, cl, slot, sub, lane, x0, nz0);
+    split_out<MODE, COUNT, OUT>(A, W, S, cl, slot, sub, lane, x0, nz0, nzt);
     if (COUNT && lane == 0) tally_out(W, ty);
+#ifdef WFPT_PHASE_TIMING
+    // split units in the upper half of the records (unit u at kPhaseWaves / 2 + u)
+    if (lane == 0 && u < kPhaseWaves / 2) {
+      unsigned long long* rec = W.phase + (kPhaseWaves / 2 + u) * 8;
+      rec[0] = rt0;
+      rec[1] = __builtin_amdgcn_s_memrealtime();
+      for (int k = 0; k < 5; ++k) rec[2 + k] = pc.ph[k];
+      rec[7] = (unsigned long long)pc.nz | ((unsigned long long)pc.nt << 32);
+    }
+#endif
     return;
   }
   if (lane == 0) {
-    record_heavy(S, c, nz0 > kHeavyZ);
+    record_heavy(S, c, heavy_class(nz0, nzt));
     if (W.redo) W.redo[c] = 0;
   }
   bool defer = oc == kExact;
@@ -860,7 +888,7 @@ __global__ __launch_bounds__(kEngBlock, WFPT_ENG_WAVES) void engine_kernel(Trial
   chunk_out<COUNT, OUT>(A, W, c, lane, p, defer, rf, oc == kTree ? (long long)cl.cnt[lane] : ne0);
   pc.mark(4);
 #ifdef WFPT_PHASE_TIMING
-  if (lane == 0 && c < kPhaseWaves) {
+  if (lane == 0 && c < kPhaseWaves / 2) {
     unsigned long long* rec = W.phase + c * 8;
     rec[0] = rt0;
     rec[1] = __builtin_amdgcn_s_memrealtime();
@@ -1231,8 +1259,12 @@ __device__ inline void fin_write(double t, long long zz, int dd, int* status, do
   out[6] = ntree;
   out[3] = (double)res3;
   // heavy chunks recorded for the next call (Split)
-  out[5] = split_rd ? (double)*split_rd : 0.0;
-  if (split_rs) *split_rs = 0;
+  out[5] = split_rd ? (double)split_rd[0] : 0.0;  // class 1 (Split)
+  out[7] = split_rd ? (double)split_rd[2] : 0.0;  // class 2
+  if (split_rs) {
+    split_rs[0] = 0;
+    split_rs[2] = 0;
+  }
   if (mirror) {  // device copy of the result (the RCCL exchange reads it)
     mirror[0] = out[0];
     mirror[1] = out[1];
@@ -1240,6 +1272,7 @@ __device__ inline void fin_write(double t, long long zz, int dd, int* status, do
     mirror[3] = out[3];
     mirror[5] = out[5];
     mirror[6] = out[6];
+    mirror[7] = out[7];
   }
   // completion word, a system-scope release store after the results (one
   // thread wrote them all): the host may poll it (acquire) instead of waiting
@@ -2747,7 +2780,7 @@ static void run_fast(const TrialArgs& A, const Work& W, const EngTables& T, cons
     hipLaunchKernelGGL((lean_kernel<MODE, COUNT, OUT>), dim3((A.n + kLeanBlock - 1) / kLeanBlock),
                        dim3(kLeanBlock), 0, s, A, W, R);
   } else {
-    const int64_t units = (int64_t)S.n * kSplit + (A.n + 63) / 64;
+    const int64_t units = (int64_t)(S.n + S.n2) * kSplit + (A.n + 63) / 64;
     hipLaunchKernelGGL((engine_kernel<MODE, COUNT, OUT>),
                        dim3((units + kEngWaves - 1) / kEngWaves), dim3(kEngBlock), 0, s, A, W, T,
                        S);

@@ -36,6 +36,9 @@ VARIANTS = {
     "direct_off": ["WFPT_DIRECT_ARGS=0"],
     "lb64": ["WFPT_LEAN_BLOCK=64"],
     "lb128": ["WFPT_LEAN_BLOCK=128"],
+    "phase": ["WFPT_PHASE_TIMING"],
+    "htot0": ["WFPT_HEAVY_TOTAL=0"],
+    "split16": ["WFPT_SPLIT=16"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
