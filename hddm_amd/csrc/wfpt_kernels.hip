@@ -960,6 +960,9 @@ template <int MODE, bool COUNT, int OUT>
 __global__ __launch_bounds__(kLeanBlock, FastWaves<MODE>::value > 0 ? FastWaves<MODE>::value : 1)
 void lean_kernel(TrialArgs A, Work W, RootGrids R) {
   exp_table_init();
+#ifdef WFPT_PHASE_TIMING
+  const long long rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
 #if WFPT_LEAN_REVERSE
   // blocks dispatched last take the first chunks (timing experiment)
   const int64_t i = (int64_t)(gridDim.x - 1 - blockIdx.x) * kLeanBlock + threadIdx.x;
@@ -1002,6 +1005,20 @@ void lean_kernel(TrialArgs A, Work W, RootGrids R) {
     return;
   }
   chunk_out<COUNT, OUT>(A, W, c, lane, p, oc == kExact, kFlagExact, ne0);
+#ifdef WFPT_PHASE_TIMING
+  // per-wave start / end (the lean pass has no split units: every record)
+  if (lane == 0 && c < kPhaseWaves) {
+    unsigned long long* rec = W.phase + c * 8;
+    rec[0] = rt0;
+    rec[1] = __builtin_amdgcn_s_memrealtime();
+    unsigned hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    rec[2] = hw;
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    rec[3] = xcc;
+  }
+#endif
 }
 
 // A node's trial term: mixture with the node's p_outlier, -inf for a zero
