@@ -39,6 +39,7 @@ VARIANTS = {
     "phase": ["WFPT_PHASE_TIMING"],
     "htot0": ["WFPT_HEAVY_TOTAL=0"],
     "split16": ["WFPT_SPLIT=16"],
+    "split4": ["WFPT_SPLIT=4"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
