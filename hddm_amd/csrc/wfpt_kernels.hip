@@ -1733,6 +1733,55 @@ __device__ inline double node_sum(const double* lp, const int64_t* off, int32_t 
   return __ballot(zero != 0) != 0ull ? -INFINITY : s;
 }
 
+// node_sum of NB nodes of one wave at once (vj[b], on[b]): the same per-node
+// operations -- each lane's strided terms in the same order, the same 0.0
+// additions past a segment's end inside an active batch, one wave_sum per
+// node -- with every node's loads issued before any node's additions, so the
+// wave waits one memory latency per batch instead of one per node.
+template <int NB>
+__device__ inline void node_sums(const double* lp, const int64_t* off, const int32_t (&vj)[NB],
+                                 const bool (&on)[NB], int32_t m, int64_t n, int lane,
+                                 double (&out)[NB]) {
+  int64_t lo[NB], hi[NB];
+  double s[NB];
+  int zero[NB];
+  int64_t len = 0;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const int tab = on[b] ? vj[b] / m : 0, jr = on[b] ? vj[b] - tab * m : 0;
+    lo[b] = on[b] ? tab * n + off[jr] : 0;
+    hi[b] = on[b] ? tab * n + off[jr + 1] : 0;
+    len = hi[b] - lo[b] > len ? hi[b] - lo[b] : len;
+    s[b] = 0.0;
+    zero[b] = 0;
+  }
+  for (int64_t q = lane; q < len; q += 256) {
+    double v[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = lo[b] + q + 64 * u;
+        v[b][u] = i < hi[b] ? lp[i] : 0.0;
+      }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      if (lo[b] + q < hi[b]) {  // node_sum's iteration i0 = lo + q is active
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (v[b][u] == -INFINITY) zero[b] = 1;
+          else s[b] += v[b][u];
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const double t = wave_sum(s[b]);
+    out[b] = __ballot(zero[b] != 0) != 0ull ? -INFINITY : t;
+  }
+}
+
 // The rare trials of a node call (rare_push), one lane each: the exact path
 // or the per-lane walk of the trial's family, its node term into lp. Launched
 // only when the publication found the list non-empty (the host re-publishes;
@@ -1812,6 +1861,11 @@ __global__ __launch_bounds__(256) void segment_sum_kernel(const double* lp, cons
 #define WFPT_PUB_BLOCKS 128
 #endif
 constexpr int32_t kPubBlocks = WFPT_PUB_BLOCKS;
+// nodes a publishing wave sums at once (node_sums; 1: one node at a time)
+#ifndef WFPT_PUB_NODES
+#define WFPT_PUB_NODES 4
+#endif
+constexpr int kPubNodes = WFPT_PUB_NODES;
 // Multi-table calls: n_nodes = T m virtual nodes, node j of table t at
 // t m + j, summing trials [t n + off[j], t n + off[j + 1]) of lp.
 // check_rare: a call whose level-0 / record / chunk kernels left rare trials
@@ -1832,11 +1886,28 @@ __global__ __launch_bounds__(256) void segment_publish_kernel(const double* lp, 
   // (written by the call's earlier kernels: stream order)
   const bool pending = check_rare && counters[1] > 0;
   double sum = 0.0;  // (the diagnostic build's: one node per wave)
-  for (int j = pending ? n_nodes : j0; j < n_nodes; j += nwv) {
+#if WFPT_PUB_DIAG
+  for (int j = pending ? n_nodes : j0; j < n_nodes; j += nwv)
     sum = node_sum(lp, off, j, m_tab, n_tab, lane);
-    if (!WFPT_PUB_DIAG && lane == 0)  // (1)
-      __hip_atomic_store(&res[j], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  // wave w sums nodes w, w + nwv, ..., kPubNodes of them at a time
+  for (int j = pending ? n_nodes : j0; j < n_nodes; j += kPubNodes * nwv) {
+    int32_t vj[kPubNodes];
+    bool on[kPubNodes];
+    double sums[kPubNodes];
+#pragma unroll
+    for (int b = 0; b < kPubNodes; ++b) {
+      vj[b] = j + b * nwv;
+      on[b] = vj[b] < n_nodes;
+    }
+    node_sums<kPubNodes>(lp, off, vj, on, m_tab, n_tab, lane, sums);
+    if (lane == 0) {  // (1)
+#pragma unroll
+      for (int b = 0; b < kPubNodes; ++b)
+        if (on[b]) __hip_atomic_store(&res[vj[b]], sums[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
+#endif
   // the storing wave waits for its agent-scope stores (and status atomics) to
   // be performed: LLVM's workgroup barrier does not wait for other waves'
   // vector memory operations (non-tgsplit gfx950 emits only lgkmcnt(0) before

@@ -40,6 +40,7 @@ VARIANTS = {
     "htot0": ["WFPT_HEAVY_TOTAL=0"],
     "split16": ["WFPT_SPLIT=16"],
     "split4": ["WFPT_SPLIT=4"],
+    "pubnodes1": ["WFPT_PUB_NODES=1"],
 }
 LIBDIR = os.path.join(ROOT, "hddm_amd", "lib", "variants")
 
